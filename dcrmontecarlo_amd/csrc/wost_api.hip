@@ -1,0 +1,673 @@
+// wost_api.hip -- host side of libwost.so: the C ABI of include/wost.h.
+//
+// Mirrors the control flow around the reference's hot loop:
+//   wost_create  <- WostSolver_2D.__init__ / buildModifiedSigma (solvers/WoStSolver.py:22-138)
+//   wost_solve   <- WostSolver_2D.solve / _solveUnified        (solvers/WoStSolver.py:162-353)
+// and owns the device state: geometry, field programs, sampler table,
+// per-walk workspace and the walk/reduce launches on a private HIP stream.
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "wost_device.h"
+#include "wost_internal.h"
+#include "wost_tables.h"
+
+using namespace wost;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(WOST_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));   \
+    } while (0)
+
+struct HostField {
+    bool present = false;
+    int flags = 0;
+    std::vector<DTerm> terms;      // first = index into this field's factors
+    std::vector<DFactor> factors;
+};
+
+int convert_field(const wost_field* in, HostField& out, const char* name) {
+    out = HostField();
+    if (!in) return WOST_OK;
+    if (in->n_terms < 0 || in->n_factors < 0 || (in->n_terms > 0 && !in->terms) ||
+        (in->n_factors > 0 && !in->factors))
+        return fail(WOST_ERR_INVALID_ARG, "field %s: bad term/factor arrays", name);
+    if (in->n_terms > 4096 || in->n_factors > 16384)
+        return fail(WOST_ERR_INVALID_ARG, "field %s: too many terms/factors", name);
+    out.present = true;
+    out.flags = in->flags;
+    for (int i = 0; i < in->n_factors; ++i) {
+        const wost_factor& f = in->factors[i];
+        if (f.kind < WOST_FK_MONO || f.kind > WOST_FK_IND_DISK)
+            return fail(WOST_ERR_INVALID_ARG, "field %s: factor %d has unknown kind %d", name, i, f.kind);
+        if (f.kind == WOST_FK_MONO) {
+            for (int q = 0; q < 2; ++q) {
+                float e = f.p[q];
+                if (!(e >= 0.f && e <= 15.f) || e != std::floor(e))
+                    return fail(WOST_ERR_INVALID_ARG, "field %s: monomial exponent %g not an integer in [0,15]", name, e);
+            }
+        }
+        DFactor d{};
+        d.kind = f.kind;
+        for (int q = 0; q < 8; ++q) d.p[q] = f.p[q];
+        out.factors.push_back(d);
+    }
+    for (int t = 0; t < in->n_terms; ++t) {
+        const wost_term& tm = in->terms[t];
+        if (tm.n_factors < 0 || tm.first_factor < 0 || tm.first_factor + tm.n_factors > in->n_factors)
+            return fail(WOST_ERR_INVALID_ARG, "field %s: term %d references factors out of range", name, t);
+        DTerm d{};
+        d.coef = tm.coef;
+        d.first = tm.first_factor;
+        d.nf = tm.n_factors;
+        out.terms.push_back(d);
+    }
+    return WOST_OK;
+}
+
+// Flattened program for the device (and for host-side evaluation).
+struct Program {
+    std::vector<unsigned char> bytes;
+    const DProgram* hdr() const { return reinterpret_cast<const DProgram*>(bytes.data()); }
+    const DTerm* terms() const { return reinterpret_cast<const DTerm*>(bytes.data() + sizeof(DProgram)); }
+    const DFactor* factors() const {
+        return reinterpret_cast<const DFactor*>(bytes.data() + sizeof(DProgram) +
+                                                sizeof(DTerm) * hdr()->n_terms_total);
+    }
+};
+
+void build_program(const HostField* f, double sigma_bar, Program& out) {
+    DProgram hdr{};
+    std::vector<DTerm> terms;
+    std::vector<DFactor> factors;
+    for (int s = 0; s < N_SLOTS; ++s) {
+        hdr.field[s].present = f[s].present ? 1 : 0;
+        hdr.field[s].flags = f[s].flags;
+        hdr.field[s].first_term = (int)terms.size();
+        hdr.field[s].n_terms = (int)f[s].terms.size();
+        const int fbase = (int)factors.size();
+        for (DTerm t : f[s].terms) {
+            t.first += fbase;
+            terms.push_back(t);
+        }
+        for (const DFactor& d : f[s].factors) factors.push_back(d);
+    }
+    fit_i0e_chebyshev(hdr.cheb_a, kChebA, hdr.cheb_b, kChebB);
+    hdr.sigma_bar = (float)sigma_bar;
+    hdr.sqrt_sigma_bar = (float)std::sqrt(sigma_bar > 0 ? sigma_bar : 0.0);
+    hdr.inv_sigma_bar = sigma_bar > 0 ? (float)(1.0 / sigma_bar) : 0.f;
+    hdr.n_terms_total = (int)terms.size();
+    out.bytes.assign(sizeof(DProgram) + sizeof(DTerm) * terms.size() + sizeof(DFactor) * factors.size(), 0);
+    std::memcpy(out.bytes.data(), &hdr, sizeof(hdr));
+    if (!terms.empty())
+        std::memcpy(out.bytes.data() + sizeof(DProgram), terms.data(), sizeof(DTerm) * terms.size());
+    if (!factors.empty())
+        std::memcpy(out.bytes.data() + sizeof(DProgram) + sizeof(DTerm) * terms.size(), factors.data(),
+                    sizeof(DFactor) * factors.size());
+}
+
+// torch.linspace(start, end, steps) in float32 (ATen CPU kernel: the first half
+// counts up from start, the second half down from end).
+std::vector<float> torch_linspace(float start, float end, int steps) {
+    std::vector<float> v(steps);
+    if (steps == 1) { v[0] = start; return v; }
+    const float step = (end - start) / (float)(steps - 1);
+    const int half = steps / 2;
+    for (int i = 0; i < steps; ++i)
+        v[i] = i < half ? start + step * (float)i : end - step * (float)(steps - i - 1);
+    return v;
+}
+
+}  // namespace
+
+struct wost_handle {
+    int device = 0;
+    int compat = WOST_COMPAT_REFERENCE;
+    int num_cus = 0;
+    std::vector<float> dverts, nverts;
+    HostField fields[N_SLOTS];
+    bool delta = false;
+    double sigma_bar = 0.0;
+    Program prog;
+    std::vector<float> table;   // sampler nodes (built on first use)
+    bool table_ready = false;
+    bool prog_dirty = true;
+
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    float2* d_dverts = nullptr;
+    float2* d_nverts = nullptr;
+    float* d_table = nullptr;
+    char* d_prog = nullptr;
+    size_t d_prog_cap = 0;
+    unsigned long long* d_counter = nullptr;
+    float* d_val = nullptr;
+    uint32_t* d_steps = nullptr;
+    int64_t ws_cap = 0;
+    int64_t* d_begin = nullptr;
+    int64_t begin_cap = 0;
+    double* d_bstats = nullptr;
+    int64_t bstats_cap = 0;
+    float2* d_points = nullptr;
+    int64_t points_cap = 0;
+    wost_timing timing{};
+};
+
+namespace {
+
+constexpr int64_t kMaxBatchWalks = int64_t(1) << 26;   // 64 Mi walks = 512 MiB of per-walk results
+
+int upload_program(wost_handle* h) {
+    if (!h->prog_dirty) return WOST_OK;
+    build_program(h->fields, h->sigma_bar, h->prog);
+    if (h->prog.bytes.size() > h->d_prog_cap) {
+        if (h->d_prog) (void)hipFree(h->d_prog);
+        h->d_prog = nullptr;
+        HIP_TRY(hipMalloc(&h->d_prog, h->prog.bytes.size()));
+        h->d_prog_cap = h->prog.bytes.size();
+    }
+    HIP_TRY(hipMemcpy(h->d_prog, h->prog.bytes.data(), h->prog.bytes.size(), hipMemcpyHostToDevice));
+    h->prog_dirty = false;
+    return WOST_OK;
+}
+
+int ensure_table(wost_handle* h) {
+    if (h->table_ready) return WOST_OK;
+    h->table.assign(WOST_SAMPLER_TABLE_N, 0.f);
+    if (h->delta)
+        screened_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N, h->sigma_bar);
+    else
+        greens_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N);
+    if (!h->d_table) HIP_TRY(hipMalloc(&h->d_table, sizeof(float) * WOST_SAMPLER_TABLE_N));
+    HIP_TRY(hipMemcpy(h->d_table, h->table.data(), sizeof(float) * WOST_SAMPLER_TABLE_N, hipMemcpyHostToDevice));
+    h->table_ready = true;
+    return WOST_OK;
+}
+
+// buildModifiedSigma's sigma_bar (solvers/WoStSolver.py:129-136 with
+// utils.py:65-120): max - min of sigma' on a 50x50 ij-grid over the bounding
+// box of all boundary vertices; NaN/inf samples skipped; a range <= 0 or
+// > 1e3 falls back to 10.0 (quirk Q8).
+double estimate_sigma_bar(const wost_handle* h, const Program& prog) {
+    float xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
+    auto scan = [&](const std::vector<float>& v) {
+        for (size_t i = 0; i + 1 < v.size(); i += 2) {
+            xmin = std::min(xmin, v[i]); xmax = std::max(xmax, v[i]);
+            ymin = std::min(ymin, v[i + 1]); ymax = std::max(ymax, v[i + 1]);
+        }
+    };
+    scan(h->dverts);
+    scan(h->nverts);
+    const std::vector<float> gx = torch_linspace(xmin, xmax, 50), gy = torch_linspace(ymin, ymax, 50);
+    const DProgram* hd = prog.hdr();
+    const DField& fa = hd->field[SLOT_ALPHA];
+    const DField& fs = hd->field[SLOT_SIGMA];
+    const bool detached = (fa.flags & WOST_FIELD_DETACHED) != 0;
+    bool any = false;
+    float lo = INFINITY, hi = -INFINITY;
+    for (float x : gx) {
+        for (float y : gy) {
+            Jet aj = field_jet(fa, prog.terms(), prog.factors(), x, y);
+            float sg = fs.present ? field_value(fs, prog.terms(), prog.factors(), x, y) : 0.f;
+            float sp = sigma_prime_from(aj, sg, detached);
+            if (std::isnan(sp) || std::isinf(sp)) continue;
+            any = true;
+            lo = std::min(lo, sp);
+            hi = std::max(hi, sp);
+        }
+    }
+    if (!any) return NAN;
+    double sb = (double)hi - (double)lo;
+    if (sb <= 0.0 || sb > 1e3) sb = 10.0;
+    return sb;
+}
+
+int walk_mode(const wost_handle* h) {
+    const bool neu = !h->nverts.empty();
+    const bool src = h->fields[SLOT_F].present;
+    if (h->delta) return neu ? MODE_MIXED_DELTA : MODE_DELTA;
+    if (neu) return src ? MODE_MIXED_POISSON : MODE_MIXED;
+    return src ? MODE_POISSON : MODE_DIRICHLET;
+}
+
+template <class T>
+int ensure_cap(T*& p, int64_t& cap, int64_t need) {
+    if (need <= cap) return WOST_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, sizeof(T) * (size_t)need);
+    if (e != hipSuccess) return fail(WOST_ERR_OOM, "hipMalloc(%lld bytes): %s", (long long)(sizeof(T) * need), hipGetErrorString(e));
+    cap = need;
+    return WOST_OK;
+}
+
+// per-walk value and step buffers, always of equal capacity
+int ensure_workspace(wost_handle* h, int64_t need) {
+    if (need <= h->ws_cap && h->d_val && h->d_steps) return WOST_OK;
+    if (h->d_val) (void)hipFree(h->d_val);
+    if (h->d_steps) (void)hipFree(h->d_steps);
+    h->d_val = nullptr;
+    h->d_steps = nullptr;
+    h->ws_cap = 0;
+    hipError_t e = hipMalloc(&h->d_val, sizeof(float) * (size_t)need);
+    if (e == hipSuccess) e = hipMalloc(&h->d_steps, sizeof(uint32_t) * (size_t)need);
+    if (e != hipSuccess) return fail(WOST_ERR_OOM, "per-walk workspace of %lld walks: %s", (long long)need, hipGetErrorString(e));
+    h->ws_cap = need;
+    return WOST_OK;
+}
+
+int check_polyline(const wost_polyline& p, const char* name, bool required, std::vector<float>& out) {
+    out.clear();
+    if (!p.xy || p.n_vertices == 0) {
+        if (required) return fail(WOST_ERR_INVALID_ARG, "%s polyline is required", name);
+        return WOST_OK;
+    }
+    if (p.n_vertices < 2) return fail(WOST_ERR_INVALID_ARG, "%s polyline needs >= 2 vertices (got %d)", name, p.n_vertices);
+    out.assign(p.xy, p.xy + 2 * (size_t)p.n_vertices);
+    for (float v : out)
+        if (!std::isfinite(v)) return fail(WOST_ERR_INVALID_ARG, "%s polyline has a non-finite coordinate", name);
+    return WOST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wost_version(void) { return WOST_ABI_VERSION; }
+
+const char* wost_last_error(void) { return g_err.c_str(); }
+
+int wost_device_count(int32_t* count) {
+    if (!count) return fail(WOST_ERR_INVALID_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(WOST_ERR_NO_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return WOST_OK;
+}
+
+int64_t wost_num_blocks(int64_t n_points, int64_t walks_per_point) {
+    if (n_points <= 0 || walks_per_point <= 0) return 0;
+    return n_points * ((walks_per_point + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS);
+}
+
+void wost_destroy(wost_handle* h) {
+    if (!h) return;
+    if (h->device >= 0) (void)hipSetDevice(h->device);
+    void* ptrs[] = {h->d_dverts, h->d_nverts, h->d_table, h->d_prog, h->d_counter, h->d_val,
+                    h->d_steps, h->d_begin, h->d_bstats, h->d_points};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    for (hipEvent_t& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int wost_create(const wost_problem* pb, wost_handle** out) {
+    if (!pb || !out) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    *out = nullptr;
+    if (pb->compat != WOST_COMPAT_REFERENCE) {
+        if (pb->compat == WOST_COMPAT_FIXED)
+            return fail(WOST_ERR_UNSUPPORTED, "compat='fixed' is not available in ABI version %d", WOST_ABI_VERSION);
+        return fail(WOST_ERR_INVALID_ARG, "unknown compat %d", pb->compat);
+    }
+    wost_handle* h = new wost_handle();
+    h->device = -1;
+    int rc;
+    if ((rc = check_polyline(pb->dirichlet, "dirichlet", true, h->dverts)) != WOST_OK ||
+        (rc = check_polyline(pb->neumann, "neumann", false, h->nverts)) != WOST_OK ||
+        (rc = convert_field(pb->boundary, h->fields[SLOT_G], "boundary")) != WOST_OK ||
+        (rc = convert_field(pb->source, h->fields[SLOT_F], "source")) != WOST_OK ||
+        (rc = convert_field(pb->sigma, h->fields[SLOT_SIGMA], "sigma")) != WOST_OK ||
+        (rc = convert_field(pb->alpha, h->fields[SLOT_ALPHA], "alpha")) != WOST_OK) {
+        delete h;
+        return rc;
+    }
+    h->compat = pb->compat;
+    // solvers/WoStSolver.py:54-64: any of sigma/alpha turns on delta tracking,
+    // the missing one defaults to sigma = 0 / alpha = 1 (constant => Q9 fallback).
+    h->delta = h->fields[SLOT_SIGMA].present || h->fields[SLOT_ALPHA].present;
+    if (h->delta) {
+        if (!h->fields[SLOT_ALPHA].present) {
+            HostField& a = h->fields[SLOT_ALPHA];
+            a.present = true;
+            a.flags = WOST_FIELD_DETACHED;
+            a.terms.push_back(DTerm{1.0f, 0, 0, 0});
+        }
+        if (!h->fields[SLOT_SIGMA].present) {
+            HostField& s = h->fields[SLOT_SIGMA];
+            s.present = true;
+            s.terms.push_back(DTerm{0.0f, 0, 0, 0});
+        }
+        if (pb->sigma_bar_override > 0.0) {
+            h->sigma_bar = pb->sigma_bar_override;
+        } else {
+            Program tmp;
+            build_program(h->fields, 1.0, tmp);
+            h->sigma_bar = estimate_sigma_bar(h, tmp);
+            if (!(h->sigma_bar > 0.0)) {
+                wost_destroy(h);
+                return fail(WOST_ERR_INVALID_ARG,
+                            "sigma' could not be evaluated at any grid point (reference raises ValueError, utils.py:108-109)");
+            }
+        }
+    }
+
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) {
+        wost_destroy(h);
+        return fail(WOST_ERR_NO_DEVICE, "no HIP device available (%s)", hipGetErrorString(e));
+    }
+    if (pb->device < 0 || pb->device >= ndev) {
+        wost_destroy(h);
+        return fail(WOST_ERR_INVALID_ARG, "device %d out of range [0,%d)", pb->device, ndev);
+    }
+    h->device = pb->device;
+#define CREATE_TRY(expr)                                              \
+    do {                                                              \
+        hipError_t e_ = (expr);                                       \
+        if (e_ != hipSuccess) {                                       \
+            int rc_ = fail(WOST_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+            wost_destroy(h);                                          \
+            return rc_;                                               \
+        }                                                             \
+    } while (0)
+    CREATE_TRY(hipSetDevice(h->device));
+    CREATE_TRY(hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, h->device));
+    CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    for (hipEvent_t& ev : h->ev) CREATE_TRY(hipEventCreate(&ev));
+    CREATE_TRY(hipMalloc(&h->d_counter, sizeof(unsigned long long)));
+    CREATE_TRY(hipMalloc(&h->d_dverts, sizeof(float) * h->dverts.size()));
+    CREATE_TRY(hipMemcpy(h->d_dverts, h->dverts.data(), sizeof(float) * h->dverts.size(), hipMemcpyHostToDevice));
+    if (!h->nverts.empty()) {
+        CREATE_TRY(hipMalloc(&h->d_nverts, sizeof(float) * h->nverts.size()));
+        CREATE_TRY(hipMemcpy(h->d_nverts, h->nverts.data(), sizeof(float) * h->nverts.size(), hipMemcpyHostToDevice));
+    }
+#undef CREATE_TRY
+    if ((rc = upload_program(h)) != WOST_OK) {
+        wost_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return WOST_OK;
+}
+
+int wost_set_field(wost_handle* h, int32_t slot, const wost_field* field) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    int s;
+    if (slot == WOST_SLOT_BOUNDARY) s = SLOT_G;
+    else if (slot == WOST_SLOT_SOURCE) s = SLOT_F;
+    else return fail(WOST_ERR_INVALID_ARG, "unknown field slot %d", slot);
+    HostField hf;
+    int rc = convert_field(field, hf, s == SLOT_G ? "boundary" : "source");
+    if (rc != WOST_OK) return rc;
+    h->fields[s] = hf;
+    h->prog_dirty = true;
+    HIP_TRY(hipSetDevice(h->device));
+    return upload_program(h);
+}
+
+int wost_get_info(const wost_handle* h, double* sigma_bar, int32_t* use_delta) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    if (sigma_bar) *sigma_bar = h->sigma_bar;
+    if (use_delta) *use_delta = h->delta ? 1 : 0;
+    return WOST_OK;
+}
+
+int wost_sampler_table(const wost_handle* hc, float* out, int32_t n) {
+    wost_handle* h = const_cast<wost_handle*>(hc);
+    if (!h || !out || n != WOST_SAMPLER_TABLE_N)
+        return fail(WOST_ERR_INVALID_ARG, "need a handle and a %d-float buffer", WOST_SAMPLER_TABLE_N);
+    HIP_TRY(hipSetDevice(h->device));
+    int rc = ensure_table(h);
+    if (rc != WOST_OK) return rc;
+    std::memcpy(out, h->table.data(), sizeof(float) * WOST_SAMPLER_TABLE_N);
+    return WOST_OK;
+}
+
+int wost_last_timing(const wost_handle* h, wost_timing* out) {
+    if (!h || !out) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    *out = h->timing;
+    return WOST_OK;
+}
+
+int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
+               int64_t block_begin, int64_t block_end, int32_t max_steps, float eps, uint64_t seed,
+               double* block_stats, double* point_stats, float* walk_values, uint32_t* walk_steps) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    if (n_points < 0 || (n_points > 0 && !points)) return fail(WOST_ERR_INVALID_ARG, "bad points");
+    if (W <= 0) return fail(WOST_ERR_INVALID_ARG, "nWalks must be >= 1 (got %lld)", (long long)W);
+    if (max_steps < 0) return fail(WOST_ERR_INVALID_ARG, "maxSteps must be >= 0");
+    if (!(eps == eps)) return fail(WOST_ERR_INVALID_ARG, "eps is NaN");
+    const int64_t nbpp = (W + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
+    const int64_t nb_total = n_points * nbpp;
+    if (block_begin < 0 || block_end < block_begin || block_end > nb_total)
+        return fail(WOST_ERR_INVALID_ARG, "block range [%lld,%lld) outside [0,%lld)", (long long)block_begin,
+                    (long long)block_end, (long long)nb_total);
+    for (int64_t i = 0; i < 2 * n_points; ++i)
+        if (!std::isfinite(points[i])) return fail(WOST_ERR_INVALID_ARG, "solve point %lld is not finite", (long long)(i / 2));
+    if (h->delta && !h->fields[SLOT_F].present)
+        return fail(WOST_ERR_INVALID_ARG,
+                    "delta tracking (sigma/alpha given) needs a source term: the reference raises "
+                    "UnboundLocalError at solvers/WoStSolver.py:281 (quirk Q14)");
+    const int mode = walk_mode(h);
+    const bool src = h->fields[SLOT_F].present;
+
+    HIP_TRY(hipSetDevice(h->device));
+    int rc;
+    if ((rc = upload_program(h)) != WOST_OK) return rc;
+    if (src && (rc = ensure_table(h)) != WOST_OK) return rc;
+
+    h->timing = wost_timing{};
+    const int64_t nblk = block_end - block_begin;
+    if (point_stats) std::fill(point_stats, point_stats + 3 * n_points, 0.0);
+    if (nblk == 0) return WOST_OK;
+
+    // block -> global walk range
+    auto blk_begin = [&](int64_t j) { return (j / nbpp) * W + (j % nbpp) * WOST_BLOCK_WALKS; };
+    auto blk_end = [&](int64_t j) {
+        const int64_t p = j / nbpp, b = j % nbpp;
+        return p * W + std::min<int64_t>((b + 1) * WOST_BLOCK_WALKS, W);
+    };
+
+    const int64_t walks_total = blk_end(block_end - 1) - blk_begin(block_begin);
+    if ((rc = ensure_cap(h->d_points, h->points_cap, std::max<int64_t>(n_points, 1))) != WOST_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(h->d_points, points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
+    if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, kMaxBatchWalks))) != WOST_OK) return rc;
+    if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * 3)) != WOST_OK) return rc;
+
+    int blocks_per_cu = 0;
+    HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), &blocks_per_cu));
+    if (blocks_per_cu < 1)
+        return fail(WOST_ERR_UNSUPPORTED, "walk kernel does not fit on a CU (polylines too large for LDS: %zu bytes)",
+                    walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2)));
+
+    WalkArgs a{};
+    a.points = h->d_points;
+    a.dverts = h->d_dverts;
+    a.nverts = h->d_nverts;
+    a.table = h->d_table;
+    a.prog = h->d_prog;
+    a.counter = h->d_counter;
+    a.walks_per_point = W;
+    a.nd = (int)(h->dverts.size() / 2);
+    a.nn = (int)(h->nverts.size() / 2);
+    a.max_steps = max_steps;
+    a.eps = eps;
+    a.rmin = eps / 2.0f;
+    a.key0 = (uint32_t)seed;
+    a.key1 = (uint32_t)(seed >> 32);
+
+    std::vector<int64_t> begins;
+    std::vector<float> ms_walk, ms_red;
+    HIP_TRY(hipEventRecord(h->ev[4], h->stream));
+    int64_t j = block_begin;
+    int64_t walks_done = 0;
+    int launches = 0;
+    double walk_ms = 0.0, red_ms = 0.0;
+    while (j < block_end) {
+        // gather whole blocks into a batch of at most kMaxBatchWalks walks
+        const int64_t wb = blk_begin(j);
+        int64_t j2 = j;
+        begins.clear();
+        while (j2 < block_end && blk_end(j2) - wb <= kMaxBatchWalks) {
+            begins.push_back(blk_begin(j2) - wb);
+            ++j2;
+        }
+        if (j2 == j) return fail(WOST_ERR_INVALID_ARG, "internal: block larger than a batch");
+        const int64_t count = blk_end(j2 - 1) - wb;
+        begins.push_back(count);
+        const int64_t nb = j2 - j;
+
+        if ((rc = ensure_cap(h->d_begin, h->begin_cap, nb + 1)) != WOST_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(h->d_begin, begins.data(), sizeof(int64_t) * (nb + 1), hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemsetAsync(h->d_counter, 0, sizeof(unsigned long long), h->stream));
+
+        a.out_val = h->d_val;
+        a.out_steps = h->d_steps;
+        a.wid_begin = wb;
+        a.count = count;
+        const int64_t max_grid = (int64_t)blocks_per_cu * h->num_cus;
+        const int64_t want = (count + kWalkBlock - 1) / kWalkBlock;
+        const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
+        const int64_t waves = (int64_t)grid * (kWalkBlock / 64);
+        a.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(1024, count / (waves * 4)));
+        h->timing.grid_blocks = grid;
+
+        HIP_TRY(hipEventRecord(h->ev[0], h->stream));
+        HIP_TRY(launch_walk(mode, a, grid, h->stream));
+        HIP_TRY(hipEventRecord(h->ev[1], h->stream));
+        HIP_TRY(launch_block_reduce(h->d_val, h->d_steps, h->d_begin, nb, h->d_bstats + 3 * (j - block_begin), h->stream));
+        HIP_TRY(hipEventRecord(h->ev[2], h->stream));
+        if (walk_values)
+            HIP_TRY(hipMemcpyAsync(walk_values + walks_done, h->d_val, sizeof(float) * count, hipMemcpyDeviceToHost, h->stream));
+        if (walk_steps)
+            HIP_TRY(hipMemcpyAsync(walk_steps + walks_done, h->d_steps, sizeof(uint32_t) * count, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipEventSynchronize(h->ev[2]));
+        float t0 = 0.f, t1 = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t0, h->ev[0], h->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&t1, h->ev[1], h->ev[2]));
+        walk_ms += t0;
+        red_ms += t1;
+        ++launches;
+        walks_done += count;
+        j = j2;
+    }
+    std::vector<double> bs(3 * nblk);
+    HIP_TRY(hipMemcpyAsync(bs.data(), h->d_bstats, sizeof(double) * 3 * nblk, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipEventRecord(h->ev[5], h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    float tt = 0.f;
+    HIP_TRY(hipEventElapsedTime(&tt, h->ev[4], h->ev[5]));
+
+    uint64_t steps_sum = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        steps_sum += (uint64_t)bs[3 * b + 2];
+        if (point_stats) {
+            const int64_t p = (block_begin + b) / nbpp;
+            point_stats[3 * p + 0] += bs[3 * b + 0];
+            point_stats[3 * p + 1] += bs[3 * b + 1];
+            point_stats[3 * p + 2] += bs[3 * b + 2];
+        }
+    }
+    if (block_stats) std::memcpy(block_stats, bs.data(), sizeof(double) * 3 * nblk);
+    h->timing.walk_kernel_ms = walk_ms;
+    h->timing.reduce_kernel_ms = red_ms;
+    h->timing.total_ms = tt;
+    h->timing.n_launches = launches;
+    h->timing.total_steps = steps_sum;
+    h->timing.total_walks = (uint64_t)walks_total;
+    return WOST_OK;
+}
+
+int wost_eval_field(wost_handle* h, int32_t which, const float* points, int64_t n, float* out) {
+    if (!h || (n > 0 && (!points || !out))) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    if (which < 0 || which > 4) return fail(WOST_ERR_INVALID_ARG, "which must be 0..4");
+    if (n == 0) return WOST_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    int rc = upload_program(h);
+    if (rc != WOST_OK) return rc;
+    float2* dp = nullptr;
+    float4* dout = nullptr;
+    HIP_TRY(hipMalloc(&dp, sizeof(float2) * n));
+    hipError_t e = hipMalloc(&dout, sizeof(float4) * n);
+    if (e == hipSuccess) e = hipMemcpyAsync(dp, points, sizeof(float2) * n, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = launch_eval_field(h->d_prog, which, dp, n, dout, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, dout, sizeof(float4) * n, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(dp);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return fail(WOST_ERR_HIP, "wost_eval_field: %s", hipGetErrorString(e));
+    return WOST_OK;
+}
+
+int wost_geometry_query(int32_t device, int32_t op, const wost_polyline* poly, const float* points,
+                        const float* dirs, const float* radii, int64_t n, float* out_f, uint8_t* out_mask) {
+    if (!poly || !poly->xy || poly->n_vertices < 1) return fail(WOST_ERR_INVALID_ARG, "bad polyline");
+    if (op < WOST_GEOM_DISTANCE || op > WOST_GEOM_INTERSECT_POLYLINES) return fail(WOST_ERR_INVALID_ARG, "unknown op %d", op);
+    const int nv = poly->n_vertices;
+    if ((op == WOST_GEOM_DISTANCE || op == WOST_GEOM_RAY_INTERSECTION || op == WOST_GEOM_INTERSECT_POLYLINES) && nv < 2)
+        return fail(WOST_ERR_INVALID_ARG, "op %d needs a polyline with >= 2 vertices", op);
+    if (n < 0 || (n > 0 && !points)) return fail(WOST_ERR_INVALID_ARG, "bad points");
+    const bool need_dirs = op == WOST_GEOM_RAY_INTERSECTION || op == WOST_GEOM_INTERSECT_POLYLINES;
+    if (need_dirs && n > 0 && !dirs) return fail(WOST_ERR_INVALID_ARG, "directions required");
+    if (op == WOST_GEOM_INTERSECT_POLYLINES && n > 0 && !radii) return fail(WOST_ERR_INVALID_ARG, "radii required");
+    const int64_t nf_out = op == WOST_GEOM_RAY_INTERSECTION ? n * (nv - 1)
+                         : op == WOST_GEOM_INTERSECT_POLYLINES ? 5 * n
+                         : op == WOST_GEOM_IS_SILHOUETTE ? 0 : n;
+    const int64_t nm_out = op == WOST_GEOM_IS_SILHOUETTE ? n * std::max(0, nv - 2) : 0;
+    if ((nf_out > 0 && !out_f) || (nm_out > 0 && !out_mask)) return fail(WOST_ERR_INVALID_ARG, "output buffer missing");
+    if (n == 0) return WOST_OK;
+    HIP_TRY(hipSetDevice(device));
+    float2 *dv = nullptr, *dp = nullptr, *dd = nullptr;
+    float *dr = nullptr, *df = nullptr;
+    uint8_t* dm = nullptr;
+    hipError_t e = hipMalloc(&dv, sizeof(float2) * nv);
+    if (e == hipSuccess) e = hipMalloc(&dp, sizeof(float2) * n);
+    if (e == hipSuccess && need_dirs) e = hipMalloc(&dd, sizeof(float2) * n);
+    if (e == hipSuccess && op == WOST_GEOM_INTERSECT_POLYLINES) e = hipMalloc(&dr, sizeof(float) * n);
+    if (e == hipSuccess && nf_out > 0) e = hipMalloc(&df, sizeof(float) * nf_out);
+    if (e == hipSuccess && nm_out > 0) e = hipMalloc(&dm, nm_out);
+    if (e == hipSuccess) e = hipMemcpy(dv, poly->xy, sizeof(float2) * nv, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dp, points, sizeof(float2) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && dd) e = hipMemcpy(dd, dirs, sizeof(float2) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && dr) e = hipMemcpy(dr, radii, sizeof(float) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_geometry_query(op, dv, nv, dp, dd, dr, n, df, dm, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess && df) e = hipMemcpy(out_f, df, sizeof(float) * nf_out, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && dm) e = hipMemcpy(out_mask, dm, nm_out, hipMemcpyDeviceToHost);
+    void* all[] = {dv, dp, dd, dr, df, dm};
+    for (void* p : all)
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(WOST_ERR_HIP, "wost_geometry_query: %s", hipGetErrorString(e));
+    return WOST_OK;
+}
+
+}  // extern "C"

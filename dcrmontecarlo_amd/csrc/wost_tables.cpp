@@ -1,0 +1,143 @@
+// wost_tables.cpp -- see wost_tables.h.
+#include "wost_tables.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace wost {
+
+static const double kPi = 3.14159265358979323846;
+
+double i0e_host(double x) {
+    x = std::fabs(x);
+    if (x == 0.0) return 1.0;
+    // integrand peaks at t = 0 with width ~ 1/sqrt(x); 4096 panels resolve
+    // x up to ~1e5, beyond that use the asymptotic series.
+    if (x > 1.0e5) {
+        double s = 1.0, term = 1.0;
+        for (int k = 1; k < 12; ++k) {
+            term *= (2.0 * k - 1.0) * (2.0 * k - 1.0) / (8.0 * k * x);
+            s += term;
+        }
+        return s / std::sqrt(2.0 * kPi * x);
+    }
+    const int m = 4096;
+    const double h = kPi / m;
+    double acc = 0.5 * (1.0 + std::exp(-2.0 * x));
+    for (int j = 1; j < m; ++j) acc += std::exp(x * (std::cos(j * h) - 1.0));
+    return acc * h / kPi;
+}
+
+double i0_host(double x) { return i0e_host(x) * std::exp(std::fabs(x)); }
+
+double k0_host(double x) {
+    if (x <= 0.0) return INFINITY;
+    if (x <= 2.0) {
+        // K0(x) = -(ln(x/2) + gamma) I0(x) + sum_{k>=1} (x^2/4)^k / (k!)^2 H_k
+        const double gamma = 0.57721566490153286061;
+        const double q = 0.25 * x * x;
+        double term = 1.0, i0 = 1.0, s = 0.0, hk = 0.0;
+        for (int k = 1; k < 40; ++k) {
+            term *= q / ((double)k * k);
+            hk += 1.0 / k;
+            i0 += term;
+            s += term * hk;
+        }
+        return -(std::log(0.5 * x) + gamma) * i0 + s;
+    }
+    // K0(x) = int_0^inf exp(-x cosh t) dt, trapezoid (spectrally accurate).
+    const double h = 0.02;
+    double acc = 0.5 * std::exp(-x);
+    for (int j = 1;; ++j) {
+        double v = std::exp(-x * std::cosh(j * h));
+        acc += v;
+        if (v < 1e-300 || (v < 1e-18 * acc)) break;
+    }
+    return acc * h;
+}
+
+static void cheb_fit(double (*g)(double), float* c, int n) {
+    std::vector<double> f(n);
+    for (int j = 0; j < n; ++j) f[j] = g(std::cos(kPi * (j + 0.5) / n));
+    for (int k = 0; k < n; ++k) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += f[j] * std::cos(kPi * k * (j + 0.5) / n);
+        s *= 2.0 / n;
+        if (k == 0) s *= 0.5;
+        c[k] = (float)s;
+    }
+}
+
+static double g_region_a(double t) { return i0e_host(4.0 * (t + 1.0)); }
+static double g_region_b(double t) {
+    double x = 16.0 / (t + 1.0);
+    return std::sqrt(x) * i0e_host(x);
+}
+
+void fit_i0e_chebyshev(float* ca, int na, float* cb, int nb) {
+    cheb_fit(g_region_a, ca, na);
+    cheb_fit(g_region_b, cb, nb);
+}
+
+double screened_greens_norm(double R, double sigma_bar) {
+    double x = R * std::sqrt(sigma_bar);
+    // 1/I0(x) = exp(-x)/i0e(x)
+    return (1.0 / sigma_bar) * (1.0 - std::exp(-x) / i0e_host(x));
+}
+
+double screened_greens(double r, double R, double sigma_bar) {
+    const double s = std::sqrt(sigma_bar);
+    const double kR = k0_host(R * s), iR = i0_host(R * s);
+    return (k0_host(r * s) - (kR / iR) * i0_host(r * s)) / (2.0 * kPi);
+}
+
+void greens_sampler_nodes(float* out, int n) {
+    const double a = 1e-6;
+    const double c0 = a - a * std::log(a);
+    const double z = 1.0 - c0;
+    auto cdf = [&](double rho) { return (rho - rho * std::log(rho) - c0) / z; };
+    for (int i = 0; i < n; ++i) {
+        const double u = (double)i / (double)(n - 1);
+        double lo = a, hi = 1.0;
+        if (i == 0) { out[i] = (float)a; continue; }
+        if (i == n - 1) { out[i] = 1.0f; continue; }
+        for (int it = 0; it < 200 && hi - lo > 1e-17; ++it) {
+            double mid = 0.5 * (lo + hi);
+            if (cdf(mid) < u) lo = mid; else hi = mid;
+        }
+        out[i] = (float)(0.5 * (lo + hi));
+    }
+}
+
+void screened_sampler_nodes(float* out, int n, double sigma_bar) {
+    const double a = 1e-6;
+    const int J = 1 << 16;
+    const double h = (1.0 - a) / J;
+    const double M = screened_greens_norm(1.0, sigma_bar);
+    const double s = std::sqrt(sigma_bar);
+    const double kR = k0_host(s), iR = i0_host(s);
+    const double ratio = kR / iR;
+    std::vector<double> p(J + 1), C(J + 1);
+    for (int j = 0; j <= J; ++j) {
+        const double rho = a + j * h;
+        const double g = std::fabs((k0_host(rho * s) - ratio * i0_host(rho * s)) / (2.0 * kPi));
+        p[j] = std::min(g, M);
+    }
+    C[0] = 0.0;
+    for (int j = 0; j < J; ++j) C[j + 1] = C[j] + 0.5 * h * (p[j] + p[j + 1]);
+    const double tot = C[J];
+    for (int i = 0; i < n; ++i) {
+        if (i == 0) { out[i] = (float)a; continue; }
+        if (i == n - 1) { out[i] = 1.0f; continue; }
+        const double target = tot * (double)i / (double)(n - 1);
+        int j = (int)(std::upper_bound(C.begin(), C.end(), target) - C.begin()) - 1;
+        j = std::max(0, std::min(j, J - 1));
+        // density linear in the cell -> CDF quadratic: A d^2 + B d = T
+        const double A = (p[j + 1] - p[j]) / (2.0 * h), B = p[j], T = target - C[j];
+        const double disc = std::sqrt(std::max(0.0, B * B + 4.0 * A * T));
+        const double d = (B + disc) > 0.0 ? 2.0 * T / (B + disc) : 0.0;
+        out[i] = (float)(a + j * h + d);
+    }
+}
+
+}  // namespace wost

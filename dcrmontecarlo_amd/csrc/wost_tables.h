@@ -1,0 +1,34 @@
+// wost_tables.h -- host-side numerics of libwost: modified Bessel functions in
+// double precision, the Chebyshev fits of i0e used by the kernel, and the
+// inverse-CDF nodes of the reference's radial samplers.
+#pragma once
+
+#include <vector>
+
+namespace wost {
+
+// i0e(x) = exp(-x) I0(x), x >= 0, ~1e-15 relative (trapezoid rule on the
+// periodic integral (1/pi) int_0^pi exp(x (cos t - 1)) dt).
+double i0e_host(double x);
+// I0(x) (may overflow to inf for x > ~700).
+double i0_host(double x);
+// K0(x), x > 0 (series for x <= 2, trapezoid on int_0^inf exp(-x cosh t) dt otherwise).
+double k0_host(double x);
+
+// Chebyshev coefficients: ca[24] for i0e on [0,8] in t = x/4-1,
+// cb[20] for sqrt(x) i0e(x) on (8,inf) in t = 16/x-1.
+void fit_i0e_chebyshev(float* ca, int na, float* cb, int nb);
+
+// screenedGreensNorm2D(R, sigma_bar) (solvers/utils.py:29-44), double.
+double screened_greens_norm(double R, double sigma_bar);
+// screenedGreens2D at distance r for ball radius R (solvers/utils.py:5-26), double.
+double screened_greens(double r, double R, double sigma_bar);
+
+// Inverse-CDF nodes F^-1(i/(n-1)), i = 0..n-1, of
+//  * GreensDistribution2D (solvers/utils.py:138-151): density -log(rho) on [1e-6, 1);
+//  * ScreenedGreensDistribution2D (solvers/utils.py:181-195): density
+//    min(|G_sigmabar(rho; R=1)|, screenedGreensNorm2D(1, sigma_bar)) on [1e-6, 1).
+void greens_sampler_nodes(float* out, int n);
+void screened_sampler_nodes(float* out, int n, double sigma_bar);
+
+}  // namespace wost

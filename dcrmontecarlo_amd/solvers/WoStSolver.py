@@ -1,0 +1,254 @@
+"""WostSolver_2D on MI355X (reference: solvers/WoStSolver.py:15-353).
+
+Drop-in for the reference class: same constructor arguments, same
+``setBoundaryConditions`` / ``setSourceTerm`` / ``solve`` signatures and
+defaults, same attributes (``use_delta_tracking``, ``sigma_bar``,
+``domain_bounds``, ``sigma_prime``). The walk loop runs in libwost's gfx950
+kernel; this class only describes the problem and moves arrays.
+
+Differences a caller sees:
+
+* Coefficient functions must be device-evaluable fields
+  (:mod:`dcrmontecarlo_amd.fields`) or numbers, not arbitrary Python callables.
+* Randomness is counter-based: ``solve(..., seed=0)`` is bitwise reproducible
+  and independent of the GPU count. Walk ``i`` of point ``p`` uses Philox
+  subsequence ``p*nWalks + i``.
+* ``solve`` returns a float32 ``[N, 1]`` array (a torch tensor if the points
+  were a torch tensor); ``return_stats=True`` adds per-point standard errors
+  and mean step counts.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from .. import _lib
+from ..fields import Field, as_field, const, detach
+
+
+def _is_torch(a) -> bool:
+    return type(a).__module__.startswith("torch")
+
+
+def _points_np(a) -> np.ndarray:
+    if _is_torch(a):
+        a = a.detach().cpu().numpy()
+    p = np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+    if p.ndim == 1 and p.shape[0] == 2:
+        p = p.reshape(1, 2)
+    if p.ndim != 2 or p.shape[1] != 2:
+        raise ValueError(f"solvePoints must have shape [N, 2], got {p.shape}")
+    return p
+
+
+def _field_or_none(f, what: str):
+    if f is None:
+        return None
+    try:
+        return as_field(f)
+    except TypeError as e:
+        raise TypeError(f"{what}: {e}") from None
+
+
+@dataclass
+class SolveStats:
+    """Per-point Monte-Carlo statistics of one solve."""
+
+    mean: np.ndarray        # [N] float64: sum / nWalks
+    stderr: np.ndarray      # [N] float64: sample std / sqrt(nWalks)
+    mean_steps: np.ndarray  # [N] float64
+    walks: int              # walks per point
+    total_steps: int
+    kernel_ms: float        # walk-kernel time (HIP events)
+    total_ms: float         # device time of the whole solve
+
+
+def stats_from_sums(sums: np.ndarray, n_walks: int, total_steps=None, kernel_ms=0.0, total_ms=0.0) -> SolveStats:
+    s, q, st = sums[:, 0], sums[:, 1], sums[:, 2]
+    mean = s / n_walks
+    var = np.maximum(q / n_walks - mean * mean, 0.0) * (n_walks / max(n_walks - 1, 1))
+    return SolveStats(mean=mean, stderr=np.sqrt(var / n_walks), mean_steps=st / n_walks, walks=n_walks,
+                      total_steps=int(st.sum()) if total_steps is None else int(total_steps),
+                      kernel_ms=float(kernel_ms), total_ms=float(total_ms))
+
+
+class WostSolver_2D:
+    """Walk-on-Stars solver for -div(alpha grad u) + sigma u = f with Dirichlet
+    and (optionally) Neumann polyline boundaries, on a HIP device."""
+
+    def __init__(self, dirichletBoundary, dirichletBoundaryFunction=None, neumannBoundary=None,
+                 source=None, sigma=None, alpha=None, *, compat: str = "reference", device: int | None = None,
+                 sigma_bar: float | None = None):
+        self.dirichletBoundary = dirichletBoundary
+        self.neumannBoundary = neumannBoundary
+        dxy = np.asarray(_np(dirichletBoundary.points), dtype=np.float32).reshape(-1, 2)
+        nxy = None if neumannBoundary is None else np.asarray(_np(neumannBoundary.points), dtype=np.float32).reshape(-1, 2)
+        allp = dxy if nxy is None else np.concatenate([dxy, nxy])
+        # solvers/WoStSolver.py:37-43
+        self.domain_bounds = [[float(allp[:, 0].min()), float(allp[:, 0].max())],
+                              [float(allp[:, 1].min()), float(allp[:, 1].max())]]
+        self.boundaryDirichlet = _field_or_none(dirichletBoundaryFunction, "dirichletBoundaryFunction")
+        self.source = _field_or_none(source, "source")
+        self.use_delta_tracking = sigma is not None or alpha is not None     # :51-64
+        self.sigma = self.alpha = None
+        if self.use_delta_tracking:
+            s = _field_or_none(sigma, "sigma")
+            a = _field_or_none(alpha, "alpha")
+            self.sigma = s if s is not None else const(0.0)                    # :55-56
+            a = a if a is not None else const(1.0)                             # :57-58
+            if a.is_constant():
+                a = detach(a)   # autograd of a constant raises -> sigma/alpha (Q9)
+            self.alpha = a
+        if compat not in _lib.COMPAT:
+            raise ValueError(f"compat must be one of {sorted(_lib.COMPAT)}")
+        self.compat = compat
+        if device is None:
+            device = int(os.environ.get("WOST_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+        self.device = int(device)
+
+        self._keep = []
+        dpoly, k1 = _lib.make_polyline(dxy)
+        npoly, k2 = _lib.make_polyline(nxy)
+        fields = {}
+        # the library applies the sigma = 0 / alpha = 1 defaults itself
+        for name, f in (("boundary", self.boundaryDirichlet), ("source", self.source),
+                        ("sigma", self.sigma if sigma is not None else None),
+                        ("alpha", self.alpha if alpha is not None else None)):
+            wf, keep = _lib.make_field(f)
+            fields[name] = ctypes.pointer(wf) if wf is not None else None
+            self._keep.append(keep)
+        prob = _lib.WostProblem(dpoly, npoly, fields["boundary"], fields["source"], fields["sigma"], fields["alpha"],
+                                _lib.COMPAT[compat], self.device, float(sigma_bar) if sigma_bar else 0.0)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.wost_create(ctypes.byref(prob), ctypes.byref(h)), "WostSolver_2D")
+        self._h = h
+        self._keep += [k1, k2]
+        sb = ctypes.c_double(0.0)
+        dt = ctypes.c_int32(0)
+        _lib.check(_lib.lib.wost_get_info(self._h, ctypes.byref(sb), ctypes.byref(dt)), "wost_get_info")
+        self.sigma_bar = float(sb.value) if self.use_delta_tracking else None
+        self.last_timing = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.lib.wost_destroy(h)
+            self._h = None
+
+    # ---- setters (solvers/WoStSolver.py:141-157) ------------------------------
+    def setBoundaryConditions(self, boundaryDirichlet):
+        self.boundaryDirichlet = _field_or_none(boundaryDirichlet, "boundaryDirichlet")
+        wf, keep = _lib.make_field(self.boundaryDirichlet)
+        _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_BOUNDARY, ctypes.pointer(wf) if wf else None),
+                   "setBoundaryConditions")
+
+    def setSourceTerm(self, source):
+        self.source = _field_or_none(source, "source")
+        wf, keep = _lib.make_field(self.source)
+        _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_SOURCE, ctypes.pointer(wf) if wf else None),
+                   "setSourceTerm")
+
+    # ---- sigma' as a callable, like the reference's attribute ----------------
+    def sigma_prime(self, point):
+        """sigma'(point) evaluated on the device (buildModifiedSigma's closure, :88-127)."""
+        p = _points_np(point)
+        out = self.eval_field("sigma_prime", p)[:, 0]
+        return out[0] if np.asarray(_np(point)).ndim == 1 else out
+
+    def eval_field(self, which: str, points) -> np.ndarray:
+        """Device evaluation: which in {g, f, sigma, alpha, sigma_prime} -> [N, 4]
+        (value, d/dx, d/dy, Laplacian; sigma_prime: sigma', alpha, sigma, 0)."""
+        idx = {"g": 0, "f": 1, "sigma": 2, "alpha": 3, "sigma_prime": 4}[which]
+        p = _points_np(points)
+        out = np.empty((p.shape[0], 4), np.float32)
+        _lib.check(_lib.lib.wost_eval_field(self._h, idx, _lib.fptr(p), p.shape[0], _lib.fptr(out)), "eval_field")
+        return out
+
+    def sampler_table(self) -> np.ndarray:
+        t = np.empty(_lib.WOST_SAMPLER_TABLE_N, np.float32)
+        _lib.check(_lib.lib.wost_sampler_table(self._h, _lib.fptr(t), t.shape[0]), "sampler_table")
+        return t
+
+    # ---- the hot path ----------------------------------------------------------
+    def solve_blocks(self, solvePoints, nWalks: int, block_begin: int, block_end: int, maxSteps: int = 1000,
+                     eps: float = 1e-4, seed: int = 0, walk_values: np.ndarray | None = None,
+                     walk_steps: np.ndarray | None = None):
+        """Run walk blocks [block_begin, block_end) (WOST_BLOCK_WALKS walks of one point
+        each) and return their (sum, sum^2, steps) rows in block order. This is
+        the unit of multi-GPU sharding (dcrmontecarlo_amd.distributed)."""
+        p = _points_np(solvePoints)
+        nb = int(block_end) - int(block_begin)
+        bs = np.zeros((max(nb, 0), 3), np.float64)
+        _lib.check(_lib.lib.wost_solve(self._h, _lib.fptr(p), p.shape[0], int(nWalks), int(block_begin),
+                                       int(block_end), int(maxSteps), float(eps), int(seed) & (2**64 - 1),
+                                       _lib.dptr(bs), None, _lib.fptr(walk_values), _lib.u32ptr(walk_steps)),
+                   "WostSolver_2D.solve")
+        self.last_timing = self.timing()
+        return bs
+
+    def num_blocks(self, n_points: int, nWalks: int) -> int:
+        return int(_lib.lib.wost_num_blocks(int(n_points), int(nWalks)))
+
+    def timing(self) -> dict:
+        t = _lib.WostTiming()
+        _lib.check(_lib.lib.wost_last_timing(self._h, ctypes.byref(t)), "wost_last_timing")
+        return {k: getattr(t, k) for k, _ in _lib.WostTiming._fields_}
+
+    def solve(self, solvePoints, nWalks=1000, maxSteps=1000, eps=1e-4, return_history=False, *,
+              seed: int = 0, return_stats: bool = False):
+        """Estimate u at each point (reference: solvers/WoStSolver.py:319-353).
+
+        Returns ``[N, 1]`` float32 (torch tensor if ``solvePoints`` is one). With
+        ``return_history=True`` returns ``(u, history)`` where history has the
+        reference's per-point list of walk dicts (``walk_id``,
+        ``total_contribution`` as the running point total like :308, plus this
+        walk's ``value`` and ``steps``; paths are not recorded). With
+        ``return_stats=True`` a :class:`SolveStats` is appended.
+        """
+        p = _points_np(solvePoints)
+        n = p.shape[0]
+        nWalks = int(nWalks)
+        if nWalks < 1:
+            raise ValueError("nWalks must be >= 1")
+        sums = np.zeros((n, 3), np.float64)
+        wv = ws = None
+        if return_history:
+            wv = np.empty(n * nWalks, np.float32)
+            ws = np.empty(n * nWalks, np.uint32)
+        nb = self.num_blocks(n, nWalks)
+        _lib.check(_lib.lib.wost_solve(self._h, _lib.fptr(p), n, nWalks, 0, nb, int(maxSteps), float(eps),
+                                       int(seed) & (2**64 - 1), None, _lib.dptr(sums), _lib.fptr(wv), _lib.u32ptr(ws)),
+                   "WostSolver_2D.solve")
+        self.last_timing = self.timing()
+        u = (sums[:, 0] / nWalks).astype(np.float32).reshape(n, 1)
+        out = [_like(u, solvePoints)]
+        if return_history:
+            hist = {}
+            for i in range(n):
+                vals = wv[i * nWalks:(i + 1) * nWalks]
+                run = np.cumsum(vals.astype(np.float64))
+                hist[i] = [{"walk_id": j, "path": [], "contributions": [], "value": float(vals[j]),
+                            "steps": int(ws[i * nWalks + j]), "total_contribution": float(run[j])}
+                           for j in range(nWalks)]
+            out.append(hist)
+        if return_stats:
+            t = self.last_timing
+            out.append(stats_from_sums(sums, nWalks, t["total_steps"], t["walk_kernel_ms"], t["total_ms"]))
+        return out[0] if len(out) == 1 else tuple(out)
+
+
+def _np(a):
+    if _is_torch(a):
+        return a.detach().cpu().numpy()
+    return np.asarray(a)
+
+
+def _like(u: np.ndarray, ref):
+    if _is_torch(ref):
+        import torch
+
+        return torch.from_numpy(u)
+    return u

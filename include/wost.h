@@ -1,0 +1,209 @@
+/*
+ * wost.h -- C ABI of libwost.so, the MI355X (gfx950) Walk-on-Stars solver.
+ *
+ * This is the drop-in boundary for the hot path of Tsuchijo/DCRMonteCarlo:
+ * the per-walk loop of WostSolver_2D._solveUnified
+ * (reference: solvers/WoStSolver.py:162-316) and the polyline queries it calls
+ * (reference: geometry/PolylinesSimple.py:25-197). The Python facade
+ * dcrmontecarlo_amd/ (WostSolver_2D, PolyLinesSimple) binds these entry points
+ * through ctypes; plain pointers and sizes only, no torch types.
+ *
+ * Every entry point returns an int status (WOST_OK == 0, negative on error);
+ * wost_last_error() returns a thread-local message for the last failure.
+ * Handles are not thread-safe; distinct handles are independent.
+ */
+#ifndef WOST_H
+#define WOST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WOST_ABI_VERSION 1
+
+/* Walks of one query point are grouped in blocks of this many consecutive
+ * walk indices. Per-block partial sums are the unit of reduction and of
+ * multi-GPU sharding (a shard is a contiguous range of blocks), which makes
+ * the result bitwise independent of the number of GPUs. */
+#define WOST_BLOCK_WALKS 4096
+
+/* Inverse-CDF table resolution of the radial source samplers. */
+#define WOST_SAMPLER_TABLE_N 4097
+
+enum wost_status {
+    WOST_OK = 0,
+    WOST_ERR_INVALID_ARG = -1,
+    WOST_ERR_HIP = -2,
+    WOST_ERR_NO_DEVICE = -3,
+    WOST_ERR_UNSUPPORTED = -4,
+    WOST_ERR_OOM = -5
+};
+
+/* compat: "reference" reproduces the reference's estimator including its
+ * quirks. "fixed" is reserved for the corrected
+ * estimator and is rejected with WOST_ERR_UNSUPPORTED in this ABI version. */
+enum wost_compat { WOST_COMPAT_REFERENCE = 0, WOST_COMPAT_FIXED = 1 };
+
+/* ---------------------------------------------------------------------------
+ * Coefficient fields. The reference takes arbitrary Python callables for the
+ * Dirichlet data g, source f, absorption sigma and diffusion alpha
+ * (solvers/WoStSolver.py:22). A GPU cannot call Python, so a field is a sum
+ * of terms, each a coefficient times a product of primitive factors:
+ *      field(x,y) = sum_t coef_t * prod_{k in t} factor_k(x,y)
+ * The factor set covers every field of the reference's scenarios
+ * (tests/testWoStCorrectness.py:81-142, tests/testWostWithSource.py:42-58,
+ *  tests/testWostVariableCoefficients.py:37-86,
+ *  tests/testGeophysicalScenario.py:11-55, utils.py:123-129, notebook cell 17)
+ * and every factor has an analytic gradient and Laplacian for sigma'.
+ * ------------------------------------------------------------------------- */
+enum wost_factor_kind {
+    WOST_FK_MONO = 1,           /* x^p0 * y^p1, p0,p1 integers in [0,15]            */
+    WOST_FK_EXP_QUAD = 2,       /* exp(p2 dx^2 + p3 dy^2 + p4 dx dy + p5 dx + p6 dy + p7),
+                                   dx = x - p0, dy = y - p1                           */
+    WOST_FK_SIN_LIN = 3,        /* sin(p0 x + p1 y + p2)                              */
+    WOST_FK_COS_LIN = 4,        /* cos(p0 x + p1 y + p2)                              */
+    WOST_FK_SIGMOID_LIN = 5,    /* 1/(1+exp(-(p0 x + p1 y + p2)))                     */
+    WOST_FK_SIGMOID_RADIAL = 6, /* 1/(1+exp(-p0 (sqrt((x-p1)^2+(y-p2)^2) - p3)))
+                                   (utils.py:123-129 torch_smooth_circle is p0=-100) */
+    WOST_FK_IND_BOX = 7,        /* 1 if p0<=x<=p1 and p2<=y<=p3 else 0 (zero gradient) */
+    WOST_FK_IND_DISK = 8        /* 1 if (x-p0)^2+(y-p1)^2 <= p2 else 0 (zero gradient) */
+};
+
+typedef struct {
+    int32_t kind;   /* enum wost_factor_kind */
+    float p[8];
+} wost_factor;
+
+typedef struct {
+    float coef;
+    int32_t first_factor;   /* index into wost_field.factors */
+    int32_t n_factors;      /* 0 => constant term */
+} wost_term;
+
+/* flags */
+#define WOST_FIELD_DETACHED 1   /* alpha only: the reference's callable returns a value
+                                   detached from autograd (or a constant), so its
+                                   sigma' falls back to sigma/alpha
+                                   (solvers/WoStSolver.py:123-127, quirk Q9). */
+
+typedef struct {
+    const wost_term* terms;
+    int32_t n_terms;
+    const wost_factor* factors;
+    int32_t n_factors;
+    int32_t flags;
+} wost_field;
+
+/* A polyline: n_vertices points, xy = [x0,y0,x1,y1,...] float32
+ * (reference: geometry/Polylines.py:14-21, points tensor [N,2]). */
+typedef struct {
+    const float* xy;
+    int32_t n_vertices;
+} wost_polyline;
+
+/* Problem description == the WostSolver_2D constructor arguments
+ * (solvers/WoStSolver.py:22-64). */
+typedef struct {
+    wost_polyline dirichlet;        /* required, >= 2 vertices                   */
+    wost_polyline neumann;          /* xy == NULL or n_vertices == 0 => none     */
+    const wost_field* boundary;     /* g; NULL => g == 0 (:45-46)                */
+    const wost_field* source;       /* f; NULL => no source term                 */
+    const wost_field* sigma;        /* NULL => 0 when alpha given (:55-56)       */
+    const wost_field* alpha;        /* NULL => 1 when sigma given (:57-58)       */
+    int32_t compat;                 /* enum wost_compat                          */
+    int32_t device;                 /* HIP device ordinal                        */
+    double sigma_bar_override;      /* > 0: use this sigma_bar instead of the
+                                       50x50 grid estimate (:130-136)            */
+} wost_problem;
+
+typedef struct wost_handle wost_handle;
+
+/* Field slots for wost_set_field. */
+enum wost_field_slot { WOST_SLOT_BOUNDARY = 0, WOST_SLOT_SOURCE = 1 };
+
+/* Timing of the last wost_solve, HIP events on the handle's stream. */
+typedef struct {
+    double walk_kernel_ms;      /* sum over launches of the walk kernel       */
+    double reduce_kernel_ms;    /* sum over launches of the block reduction    */
+    double total_ms;            /* upload -> results on host                    */
+    int32_t n_launches;         /* walk-kernel launches (batches)               */
+    int32_t grid_blocks;        /* workgroups per walk-kernel launch            */
+    uint64_t total_steps;       /* walk-steps executed in the last solve         */
+    uint64_t total_walks;
+} wost_timing;
+
+int wost_version(void);
+const char* wost_last_error(void);
+int wost_device_count(int32_t* count);
+
+/* WostSolver_2D.__init__ (solvers/WoStSolver.py:22-64): validates, estimates
+ * sigma_bar like buildModifiedSigma (:66-138), builds the radial sampler
+ * (solvers/utils.py:120-195) and uploads geometry and fields to the device. */
+int wost_create(const wost_problem* problem, wost_handle** out);
+void wost_destroy(wost_handle* h);
+
+/* setBoundaryConditions (:141-148) / setSourceTerm (:150-157). Setting a
+ * source on a problem without one changes the kernel variant used. */
+int wost_set_field(wost_handle* h, int32_t slot, const wost_field* field);
+
+/* The solver's sigma_bar (reference attribute WostSolver_2D.sigma_bar) and
+ * whether delta tracking is on (attribute use_delta_tracking). */
+int wost_get_info(const wost_handle* h, double* sigma_bar, int32_t* use_delta_tracking);
+
+/* Number of reduction blocks of a solve: n_points * ceil(walks_per_point / WOST_BLOCK_WALKS). */
+int64_t wost_num_blocks(int64_t n_points, int64_t walks_per_point);
+
+/* _solveUnified (solvers/WoStSolver.py:162-316) over the global walk blocks
+ * [block_begin, block_end) (pass 0, wost_num_blocks(...) for a full solve).
+ * Walk w of point p has global id p*walks_per_point + w; its random stream is
+ * Philox4x32-10 keyed by seed, subsequence = global id, one draw per step.
+ *
+ * Outputs (host memory, caller-owned; any may be NULL):
+ *   block_stats [n_blocks_in_range][3] : sum, sum of squares, steps per block
+ *   point_stats [n_points][3]          : the same, summed over the range's
+ *                                        blocks in block order
+ *   walk_values / walk_steps           : per-walk estimate and step count for
+ *                                        every walk in the range (walk order)
+ * Blocking; the result is bitwise reproducible for a given seed. */
+int wost_solve(wost_handle* h, const float* points, int64_t n_points,
+               int64_t walks_per_point, int64_t block_begin, int64_t block_end,
+               int32_t max_steps, float eps, uint64_t seed,
+               double* block_stats, double* point_stats,
+               float* walk_values, uint32_t* walk_steps);
+
+int wost_last_timing(const wost_handle* h, wost_timing* out);
+
+/* Device evaluation of the handle's fields at points (for tests and for the
+ * host API): which = 0 g, 1 f, 2 sigma, 3 alpha (value, d/dx, d/dy, Laplacian
+ * per point -> out[n][4]), 4 sigma' (solvers/WoStSolver.py:88-127 -> out[n][4],
+ * value in column 0). */
+int wost_eval_field(wost_handle* h, int32_t which, const float* points, int64_t n, float* out);
+
+/* The radial sampler's inverse-CDF nodes (WOST_SAMPLER_TABLE_N floats). */
+int wost_sampler_table(const wost_handle* h, float* out, int32_t n);
+
+/* Batched polyline queries on the device (geometry/PolylinesSimple.py).
+ *   op 0 distance          (:25-49, :214-224)   out_f[n]
+ *   op 1 isSilhouette      (:51-81, :242-253)   out_mask[n][nv-2]
+ *   op 2 silhouetteDistance(:83-102, :255-265)  out_f[n]
+ *   op 3 rayIntersection   (:104-132, :281-292) out_f[n][nv-1]  (dirs used)
+ *   op 4 intersectPolylines(:134-197, :294-307) out_f[n][5] = x, y, nx, ny, found
+ *                                                (dirs and radii used)   */
+enum wost_geom_op {
+    WOST_GEOM_DISTANCE = 0,
+    WOST_GEOM_IS_SILHOUETTE = 1,
+    WOST_GEOM_SILHOUETTE_DISTANCE = 2,
+    WOST_GEOM_RAY_INTERSECTION = 3,
+    WOST_GEOM_INTERSECT_POLYLINES = 4
+};
+int wost_geometry_query(int32_t device, int32_t op, const wost_polyline* poly,
+                        const float* points, const float* dirs, const float* radii,
+                        int64_t n, float* out_f, uint8_t* out_mask);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WOST_H */

@@ -1,0 +1,191 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes front end of the CPU oracle (liboracle.so).
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+checker; the product package never imports it. See wost_oracle.h for what the
+oracle restates and how it is pinned to the reference.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_double, c_float, c_int32, c_int64, c_uint8, c_uint32, c_uint64
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+class OrcFactor(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("p", c_float * 8)]
+
+
+class OrcTerm(ctypes.Structure):
+    _fields_ = [("coef", c_float), ("first_factor", c_int32), ("n_factors", c_int32)]
+
+
+class OrcField(ctypes.Structure):
+    _fields_ = [("terms", POINTER(OrcTerm)), ("n_terms", c_int32), ("factors", POINTER(OrcFactor)),
+                ("n_factors", c_int32), ("flags", c_int32)]
+
+
+class OrcProblem(ctypes.Structure):
+    _fields_ = [("dxy", POINTER(c_float)), ("nd", c_int32), ("nxy", POINTER(c_float)), ("nn", c_int32),
+                ("g", POINTER(OrcField)), ("f", POINTER(OrcField)), ("sigma", POINTER(OrcField)),
+                ("alpha", POINTER(OrcField)), ("sigma_bar", c_double)]
+
+
+def build():
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    fp = POINTER(c_float)
+    lib.orc_distance.restype = c_float
+    lib.orc_distance.argtypes = [fp, c_int32, c_float, c_float]
+    lib.orc_silhouette_distance.restype = c_float
+    lib.orc_silhouette_distance.argtypes = [fp, c_int32, c_float, c_float]
+    lib.orc_is_silhouette.argtypes = [fp, c_int32, c_float, c_float, POINTER(c_uint8)]
+    lib.orc_ray_intersection.argtypes = [fp, c_int32, c_float, c_float, c_float, c_float, fp]
+    lib.orc_intersect_polylines.argtypes = [fp, c_int32, c_float, c_float, c_float, c_float, c_float, fp]
+    lib.orc_i0.restype = c_double
+    lib.orc_i0.argtypes = [c_double]
+    lib.orc_k0.restype = c_double
+    lib.orc_k0.argtypes = [c_double]
+    lib.orc_screened_norm.restype = c_double
+    lib.orc_screened_norm.argtypes = [c_double, c_double]
+    lib.orc_sampler_nodes.argtypes = [c_int32, c_double, fp, c_int32]
+    lib.orc_field_value.restype = c_float
+    lib.orc_field_value.argtypes = [POINTER(OrcField), c_float, c_float]
+    lib.orc_sigma_prime.restype = c_float
+    lib.orc_sigma_prime.argtypes = [POINTER(OrcProblem), c_float, c_float]
+    lib.orc_sigma_bar.restype = c_double
+    lib.orc_sigma_bar.argtypes = [POINTER(OrcProblem)]
+    lib.orc_philox.argtypes = [POINTER(c_uint32), c_uint32, c_uint32, POINTER(c_uint32)]
+    lib.orc_solve.restype = c_int32
+    lib.orc_solve.argtypes = [POINTER(OrcProblem), fp, c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
+                              c_uint64, c_int32, fp, POINTER(c_uint32)]
+    return lib
+
+
+lib = _load()
+
+
+def _f(a):
+    return a.ctypes.data_as(POINTER(c_float))
+
+
+def make_field(field):
+    """dcrmontecarlo_amd.fields.Field -> (OrcField, keepalive) -- the shared problem encoding."""
+    if field is None:
+        return None, None
+    terms, factors = field.pack()
+    T = (OrcTerm * max(1, len(terms)))()
+    for i, (c, first, n) in enumerate(terms):
+        T[i].coef, T[i].first_factor, T[i].n_factors = np.float32(c), first, n
+    Fa = (OrcFactor * max(1, len(factors)))()
+    for i, (k, p) in enumerate(factors):
+        Fa[i].kind = k
+        for j in range(8):
+            Fa[i].p[j] = np.float32(p[j])
+    of = OrcField(ctypes.cast(T, POINTER(OrcTerm)), len(terms), ctypes.cast(Fa, POINTER(OrcFactor)), len(factors),
+                  field.flags)
+    return of, (T, Fa, of)
+
+
+class Problem:
+    """An oracle problem built from geometry arrays and fields (None = absent)."""
+
+    def __init__(self, dirichlet, neumann=None, g=None, f=None, sigma=None, alpha=None, sigma_bar=0.0):
+        self._d = np.ascontiguousarray(dirichlet, np.float32).reshape(-1, 2)
+        self._n = None if neumann is None else np.ascontiguousarray(neumann, np.float32).reshape(-1, 2)
+        self._keep = []
+        ptrs = []
+        for fld in (g, f, sigma, alpha):
+            of, keep = make_field(fld)
+            self._keep.append(keep)
+            ptrs.append(ctypes.pointer(of) if of is not None else None)
+        self.p = OrcProblem(_f(self._d), self._d.shape[0], _f(self._n) if self._n is not None else None,
+                            0 if self._n is None else self._n.shape[0], *ptrs, float(sigma_bar))
+
+    @classmethod
+    def from_scenario(cls, sc, sigma_bar=0.0):
+        return cls(sc.dirichlet, sc.neumann, sc.g, sc.f, sc.sigma, sc.alpha, sigma_bar)
+
+    def sigma_bar(self) -> float:
+        return float(lib.orc_sigma_bar(ctypes.byref(self.p)))
+
+    def sigma_prime(self, pts) -> np.ndarray:
+        pts = np.asarray(pts, np.float32).reshape(-1, 2)
+        return np.array([lib.orc_sigma_prime(ctypes.byref(self.p), float(x), float(y)) for x, y in pts], np.float32)
+
+    def solve_walks(self, points, n_walks, max_steps, eps, seed, wid_begin=0, wid_end=None, threads=0):
+        """Per-walk (values f32, steps u32) for global walks [wid_begin, wid_end)."""
+        pts = np.ascontiguousarray(points, np.float32).reshape(-1, 2)
+        if wid_end is None:
+            wid_end = pts.shape[0] * int(n_walks)
+        n = int(wid_end) - int(wid_begin)
+        v = np.empty(n, np.float32)
+        s = np.empty(n, np.uint32)
+        rc = lib.orc_solve(ctypes.byref(self.p), _f(pts), pts.shape[0], int(n_walks), int(wid_begin), int(wid_end),
+                           int(max_steps), float(eps), int(seed) & (2**64 - 1), int(threads), _f(v),
+                           s.ctypes.data_as(POINTER(c_uint32)))
+        if rc != 0:
+            raise ValueError(f"orc_solve failed ({rc})")
+        return v, s
+
+    def solve(self, points, n_walks, max_steps, eps, seed, threads=0):
+        """Per-point (mean, stderr, mean_steps) in float64."""
+        v, s = self.solve_walks(points, n_walks, max_steps, eps, seed, threads=threads)
+        v = v.astype(np.float64).reshape(-1, n_walks)
+        s = s.astype(np.float64).reshape(-1, n_walks)
+        se = v.std(axis=1, ddof=1) / np.sqrt(n_walks) if n_walks > 1 else np.zeros(v.shape[0])
+        return v.mean(axis=1), se, s.mean(axis=1)
+
+
+def field_value(field, pts) -> np.ndarray:
+    of, keep = make_field(field)
+    pts = np.asarray(pts, np.float32).reshape(-1, 2)
+    return np.array([lib.orc_field_value(ctypes.byref(of), float(x), float(y)) for x, y in pts], np.float32)
+
+
+def geometry(op, verts, points, dirs=None, radii=None):
+    V = np.ascontiguousarray(verts, np.float32).reshape(-1, 2)
+    P = np.asarray(points, np.float32).reshape(-1, 2)
+    nv = V.shape[0]
+    out = []
+    for i, (x, y) in enumerate(P):
+        if op == "distance":
+            out.append(lib.orc_distance(_f(V), nv, x, y))
+        elif op == "silhouetteDistance":
+            out.append(lib.orc_silhouette_distance(_f(V), nv, x, y))
+        elif op == "isSilhouette":
+            m = np.zeros(max(nv - 2, 0), np.uint8)
+            lib.orc_is_silhouette(_f(V), nv, x, y, m.ctypes.data_as(POINTER(c_uint8)))
+            out.append(m)
+        elif op == "rayIntersection":
+            t = np.zeros(nv - 1, np.float32)
+            lib.orc_ray_intersection(_f(V), nv, x, y, float(dirs[i][0]), float(dirs[i][1]), _f(t))
+            out.append(t)
+        elif op == "intersectPolylines":
+            o = np.zeros(5, np.float32)
+            lib.orc_intersect_polylines(_f(V), nv, x, y, float(dirs[i][0]), float(dirs[i][1]), float(radii[i]), _f(o))
+            out.append(o)
+    return np.array(out, dtype=np.uint8 if op == "isSilhouette" else np.float32)
+
+
+def sampler_nodes(screened: bool, sigma_bar: float = 0.0, n: int = 4097) -> np.ndarray:
+    out = np.empty(n, np.float32)
+    lib.orc_sampler_nodes(1 if screened else 0, float(sigma_bar), _f(out), n)
+    return out
+
+
+def philox(ctr, k0, k1):
+    c = (c_uint32 * 4)(*[int(v) & 0xFFFFFFFF for v in ctr])
+    o = (c_uint32 * 4)()
+    lib.orc_philox(c, c_uint32(k0), c_uint32(k1), o)
+    return tuple(int(v) for v in o)

@@ -1,0 +1,493 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE
+(Tsuchijo/DCRMonteCarlo, mounted read-only at /root/reference) in the build
+container.
+
+This script is never imported by tests and never travels to the GPU box; only
+its outputs (small .npz/.json files: inputs and expected outputs) are
+committed. It imports the reference's own modules and scenario callables and
+records what they compute:
+
+  geometry_kats.npz   PolyLinesSimple queries on every scenario geometry (G1)
+  fields_<sc>.npz     g, f, alpha, sigma, sigma' at sample points and sigma_bar (G2, G7)
+  greens.npz          screenedGreensNorm2D / screenedGreens2D tables (G3)
+  sampler_draws.npz   draws of GreensDistribution2D / ScreenedGreensDistribution2D (G4)
+  replay_<sc>.npz     per-walk results of the reference's _solveUnified with its
+                      random draws taken from the Philox stream of libwost (G5)
+  stats_<sc>.npz      per-point mean / stderr with the reference's own RNG (G6)
+
+Usage:  python tools/gen_fixtures.py [--only geometry,fields,...] [--stats-workers 8]
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import json
+import math
+import os
+import sys
+import time
+
+sys.dont_write_bytecode = True          # never write into /root/reference
+os.environ.setdefault("MPLBACKEND", "Agg")
+REF = os.environ.get("WOST_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+import scipy.special as sps  # noqa: E402
+import torch  # noqa: E402
+
+import solvers.WoStSolver as ref_mod  # noqa: E402
+import solvers.utils as ref_sutils  # noqa: E402
+from geometry.PolylinesSimple import PolyLinesSimple as RefPoly  # noqa: E402
+from solvers.WoStSolver import WostSolver_2D as RefSolver  # noqa: E402
+
+sys.path.append(REPO)
+from dcrmontecarlo_amd import scenarios as S  # noqa: E402
+
+M32 = 0xFFFFFFFF
+TABLE_N = 4097
+
+
+# ---------------------------------------------------------------------------
+# Philox4x32-10 (same stream as libwost / rocRAND: subsequence = walk id)
+# ---------------------------------------------------------------------------
+def philox(ctr, k0, k1):
+    c0, c1, c2, c3 = ctr
+    for _ in range(10):
+        p0 = 0xD2511F53 * c0
+        p1 = 0xCD9E8D57 * c2
+        c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & M32, p1 & M32, ((p0 >> 32) ^ c3 ^ k1) & M32, p0 & M32
+        k0 = (k0 + 0x9E3779B9) & M32
+        k1 = (k1 + 0xBB67AE85) & M32
+    return c0, c1, c2, c3
+
+
+def u01(v):
+    return np.float32((v >> 8) * (1.0 / 16777216.0))
+
+
+# ---------------------------------------------------------------------------
+# inverse-CDF nodes of the reference samplers (scipy, double precision)
+# ---------------------------------------------------------------------------
+def greens_nodes(n=TABLE_N):
+    a = 1e-6
+    c0 = a - a * math.log(a)
+    z = 1.0 - c0
+    out = np.empty(n, np.float32)
+    for i in range(n):
+        u = i / (n - 1)
+        lo, hi = a, 1.0
+        for _ in range(100):
+            mid = 0.5 * (lo + hi)
+            if (mid - mid * math.log(mid) - c0) / z < u:
+                lo = mid
+            else:
+                hi = mid
+        out[i] = 0.5 * (lo + hi)
+    out[0], out[-1] = a, 1.0
+    return out
+
+
+def screened_nodes(sigma_bar, n=TABLE_N):
+    a = 1e-6
+    s = math.sqrt(sigma_bar)
+    M = (1.0 / sigma_bar) * (1.0 - 1.0 / sps.i0(s))
+    J = 1 << 20
+    rho = np.linspace(a, 1.0, J + 1)
+    g = np.abs((sps.k0(rho * s) - sps.k0(s) / sps.i0(s) * sps.i0(rho * s)) / (2 * math.pi))
+    p = np.minimum(g, M)
+    C = np.concatenate([[0.0], np.cumsum(0.5 * (p[1:] + p[:-1]) * np.diff(rho))])
+    T = C[-1] * np.arange(n) / (n - 1)
+    j = np.clip(np.searchsorted(C, T, side="right") - 1, 0, J - 1)
+    h = rho[j + 1] - rho[j]
+    A = (p[j + 1] - p[j]) / (2 * h)
+    B = p[j]
+    R = T - C[j]
+    d = np.where(B + np.sqrt(np.maximum(B * B + 4 * A * R, 0)) > 0, 2 * R / (B + np.sqrt(np.maximum(B * B + 4 * A * R, 0))), 0)
+    out = (rho[j] + d).astype(np.float32)
+    out[0], out[-1] = a, 1.0
+    return out
+
+
+def lerp_node(nodes, u):
+    pos = np.float32(u) * np.float32(TABLE_N - 1)
+    i = min(int(pos), TABLE_N - 2)
+    f = np.float32(pos - np.float32(i))
+    return np.float32(nodes[i] + f * (nodes[i + 1] - nodes[i]))
+
+
+# ---------------------------------------------------------------------------
+# the reference's scenarios with the reference's own callables
+# ---------------------------------------------------------------------------
+def _quiet():
+    return contextlib.redirect_stdout(io.StringIO())
+
+
+def ref_scenarios():
+    import tests.testGeophysicalScenario as tg
+    import tests.testWoStCorrectness as tc
+    import tests.testWostVariableCoefficients as tv
+    import tests.testWostWithSource as ts
+    from utils import torch_smooth_circle
+
+    out = {}
+
+    def laplace():
+        sq = torch.tensor([[0.0, 0.0], [1.0, 0.0], [1.0, 1.0], [0.0, 1.0], [0.0, 0.0]])
+        return dict(D=RefPoly(sq), N=None, g=lambda p: p[0] ** 2 - p[1] ** 2, f=None, sigma=None, alpha=None)
+
+    out["laplace_square"] = laplace
+
+    def manufactured():
+        _, D, absorption, bc, src = tc.manufactured_solution_with_polynomial()
+        return dict(D=tc.create_square_domain(2.0), N=None, g=bc, f=src, sigma=absorption, alpha=D)
+
+    out["manufactured_polynomial"] = manufactured
+
+    def poisson():
+        dirichlet, _ = ts.create_test_domain()
+        bc, src = ts.define_boundary_conditions()
+        return dict(D=dirichlet, N=None, g=bc, f=src, sigma=None, alpha=None)
+
+    out["poisson_square"] = poisson
+
+    def varcoef():
+        dirichlet, neumann = tv.create_test_domain()
+        diff, absorb = tv.define_variable_coefficients()
+        bc, src = tv.define_boundary_conditions_and_source()
+        return dict(D=dirichlet, N=neumann, g=bc, f=src, sigma=absorb, alpha=diff)
+
+    out["variable_coefficients"] = varcoef
+
+    def dcr():
+        h = 100.0
+        dp = torch.tensor([[-h, -h], [h, -h], [h, h], [-h, h], [-h, -h]])
+        npts = torch.tensor([[-h, h], [h, h]])
+        return dict(D=RefPoly(dp), N=RefPoly(npts), g=lambda p: 0.0, f=tg.dcr_current_source, sigma=None,
+                    alpha=tg.conductivity_field)
+
+    out["dcr_dipole"] = dcr
+
+    def notebook():
+        nb = json.load(open(os.path.join(REF, "tests", "testNotebook.ipynb")))
+        ns = {"torch": torch, "torch_smooth_circle": torch_smooth_circle, "np": np}
+        exec("".join(nb["cells"][17]["source"]), ns)   # conductivity_field_torch, dcr_current_source_torch
+        dp = torch.tensor([[-500.0, 1], [-500.0, -1000.0], [500.0, -1000.0], [500.0, 1]])
+        npts = torch.tensor([[500.0, 1], [-500.0, 1]])
+        return dict(D=RefPoly(dp), N=RefPoly(npts), g=lambda p: 0.0, f=ns["dcr_current_source_torch"], sigma=None,
+                    alpha=ns["conductivity_field_torch"])
+
+    out["notebook_dcr"] = notebook
+    return out
+
+
+def build_ref_solver(spec):
+    with _quiet():
+        s = RefSolver(spec["D"], spec["g"], spec["N"], source=spec["f"], sigma=spec["sigma"], alpha=spec["alpha"])
+    return s
+
+
+# ---------------------------------------------------------------------------
+def gen_geometry():
+    rng = np.random.default_rng(7)
+    geoms = {
+        "unit_square": np.array([[0, 0], [1, 0], [1, 1], [0, 1], [0, 0]], np.float32),
+        "square2": S._square(2.0),
+        "square15": S._square(1.5),
+        "circle33": S.variable_coefficients(n_points=1, n_walks=1).neumann,
+        "box100": S.dcr_dipole(n_electrodes=1, n_walks=1).dirichlet,
+        "top_segment": S.dcr_dipole(n_electrodes=1, n_walks=1).neumann,
+        "open_u": S.notebook_dcr(1).dirichlet,
+        "zigzag": np.array([[0, 0], [1, 1], [2, 0], [3, 1.5], [3, 1.5], [4, -1], [5, 0.5]], np.float32),
+        "kat_tri": np.array([[0, 0], [1, 1], [2, 0]], np.float32),
+        "topo10k": S.topography(10_000),
+    }
+    # reference circle built by the reference itself (torch cos/sin)
+    import tests.testWostVariableCoefficients as tv
+    geoms["circle33"] = tv.create_test_domain()[1].points.numpy().astype(np.float32)
+    out = {}
+    for name, V in geoms.items():
+        lo, hi = V.min(0), V.max(0)
+        span = np.maximum(hi - lo, 1.0)
+        nq = 48 if name == "topo10k" else 256
+        P = (lo - 0.25 * span + rng.random((nq, 2)) * 1.5 * span).astype(np.float32)
+        if name == "kat_tri":
+            P[0] = (1.5, 0.6)
+        if name == "unit_square":
+            P[0] = (0.5, 0.5)
+        th = rng.random(nq) * 2 * np.pi
+        Dd = np.stack([np.cos(th), np.sin(th)], 1).astype(np.float32)
+        Dd[::7] *= np.float32(3.0)          # unnormalised directions too
+        if name == "unit_square":
+            Dd[0] = (1.0, 0.0)
+        R = (rng.random(nq) * span.max()).astype(np.float32)
+        poly = RefPoly(torch.from_numpy(V))
+        dist, sil, sild, ray, ip = [], [], [], [], []
+        for q in range(nq):
+            p = torch.from_numpy(P[q])
+            d = torch.from_numpy(Dd[q])
+            dist.append(float(poly.distance(p)))
+            sil.append(poly.isSilhouette(p).numpy().astype(np.uint8))
+            sild.append(float(poly.silhouetteDistance(p)))
+            ray.append(poly.rayIntersection(p, d).numpy())
+            xp, nrm, found = poly.intersectPolylines(p, d, float(R[q]))
+            ip.append(np.concatenate([xp.numpy(), nrm.numpy().astype(np.float32), [np.float32(bool(found))]]))
+        out[f"{name}__verts"] = V
+        out[f"{name}__points"] = P
+        out[f"{name}__dirs"] = Dd
+        out[f"{name}__radii"] = R
+        out[f"{name}__distance"] = np.array(dist, np.float32)
+        out[f"{name}__is_silhouette"] = np.array(sil, np.uint8).reshape(nq, max(len(V) - 2, 0))
+        out[f"{name}__silhouette_distance"] = np.array(sild, np.float32)
+        out[f"{name}__ray_intersection"] = np.array(ray, np.float32).reshape(nq, len(V) - 1)
+        out[f"{name}__intersect"] = np.array(ip, np.float32)
+    np.savez_compressed(os.path.join(OUT, "geometry_kats.npz"), **out)
+    print("geometry_kats.npz", len(geoms), "geometries")
+
+
+def gen_fields():
+    specs = ref_scenarios()
+    rng = np.random.default_rng(11)
+    for name in ["laplace_square", "manufactured_polynomial", "poisson_square", "variable_coefficients",
+                 "dcr_dipole", "notebook_dcr"]:
+        spec = specs[name]()
+        V = spec["D"].points.numpy()
+        if spec["N"] is not None:
+            V = np.concatenate([V, spec["N"].points.numpy()])
+        lo, hi = V.min(0), V.max(0)
+        P = (lo + rng.random((256, 2)) * (hi - lo)).astype(np.float32)
+        res = {"points": P, "dirichlet": spec["D"].points.numpy().astype(np.float32)}
+        if spec["N"] is not None:
+            res["neumann"] = spec["N"].points.numpy().astype(np.float32)
+        for key in ("g", "f", "sigma", "alpha"):
+            fn = spec[key]
+            if fn is None:
+                continue
+            vals = []
+            for p in P:
+                v = fn(torch.from_numpy(p.copy()))
+                vals.append(float(v))
+            res[key] = np.array(vals, np.float64)
+        solver = build_ref_solver(spec)
+        if solver.use_delta_tracking:
+            res["sigma_bar"] = np.float64(solver.sigma_bar)
+            sp = []
+            with _quiet():
+                for p in P:
+                    sp.append(float(solver.sigma_prime(torch.from_numpy(p.copy()))))
+            res["sigma_prime"] = np.array(sp, np.float64)
+        np.savez_compressed(os.path.join(OUT, f"fields_{name}.npz"), **res)
+        print(f"fields_{name}.npz", "sigma_bar", res.get("sigma_bar"))
+
+
+def gen_greens():
+    R = np.logspace(-3, 2.5, 60)
+    sbs = np.array([0.5, 2.40625, 3.217497, 10.0])
+    tab = np.array([[ref_sutils.screenedGreensNorm2D(float(r), float(sb)) for r in R] for sb in sbs], np.float64)
+    gn = np.array([ref_sutils.greensFunctionNorm2D(float(r)) for r in R])
+    rr = np.linspace(0.01, 0.99, 50)
+    sg = np.array([[abs(float(ref_sutils.screenedGreens2D(torch.zeros(2), torch.tensor([float(r), 0.0]), 1.0, float(sb))))
+                    for r in rr] for sb in sbs])
+    np.savez_compressed(os.path.join(OUT, "greens.npz"), R=R, sigma_bar=sbs, screened_norm=tab, greens_norm=gn,
+                        rho=rr, screened_greens_unit=sg)
+    print("greens.npz")
+
+
+def gen_sampler_draws(n=20000):
+    out = {}
+    np.random.seed(1)
+    d = ref_sutils.GreensDistribution2D(cache_size=n)
+    out["greens"] = np.array([d.sample(None, 1.0) for _ in range(n)], np.float64)
+    for sb in (2.40625, 3.217497, 10.0, 0.5):
+        np.random.seed(2)
+        d = ref_sutils.ScreenedGreensDistribution2D(sb, cache_size=n)
+        out[f"screened_{sb}"] = np.array([float(d.sample(None, 1.0)) for _ in range(n)], np.float64)
+        print("sampler", sb)
+    np.savez_compressed(os.path.join(OUT, "sampler_draws.npz"), **out)
+
+
+# ---------------------------------------------------------------------------
+# G5: replay the reference on the Philox stream
+# ---------------------------------------------------------------------------
+def replay(name, points, n_walks, max_steps, eps, seed):
+    spec = ref_scenarios()[name]()
+    solver = build_ref_solver(spec)
+    k0, k1 = seed & M32, (seed >> 32) & M32
+    st = {"wid": 0, "step": -1, "nrand": 0}
+    cache = {}
+
+    def draw():
+        key = (st["wid"], st["step"])
+        if key not in cache:
+            cache.clear()
+            w = st["wid"]
+            cache[key] = philox((st["step"] & M32, 0, w & M32, (w >> 32) & M32), k0, k1)
+        return cache[key]
+
+    D = solver.dirichletBoundary
+    orig_dist = D.distance
+
+    def distance(p):
+        st["step"] += 1
+        st["nrand"] = 0
+        return orig_dist(p)
+
+    D.distance = distance
+    orig_bc = solver.boundaryDirichlet
+
+    def bc(p):
+        v = orig_bc(p)
+        st["wid"] += 1
+        st["step"] = -1
+        return v
+
+    solver.boundaryDirichlet = bc
+    nodes = screened_nodes(solver.sigma_bar) if solver.use_delta_tracking else greens_nodes()
+
+    class FakeSampler:
+        def __init__(self, *a, **k):
+            pass
+
+        def sample(self, center, radius):
+            rho = lerp_node(nodes, u01(draw()[1]))
+            return float(rho) * radius
+
+    orig_rand = torch.rand
+
+    def fake_rand(*a, **k):
+        r = draw()
+        lane = 0 if st["nrand"] == 0 else 2
+        st["nrand"] += 1
+        return torch.tensor([float(u01(r[lane]))], dtype=torch.float32)
+
+    oG, oS = ref_mod.GreensDistribution2D, ref_mod.ScreenedGreensDistribution2D
+    ref_mod.GreensDistribution2D = FakeSampler
+    ref_mod.ScreenedGreensDistribution2D = FakeSampler
+    torch.rand = fake_rand
+    try:
+        with _quiet(), contextlib.redirect_stderr(io.StringIO()):
+            u, hist = solver.solve(torch.from_numpy(points), nWalks=n_walks, maxSteps=max_steps, eps=eps,
+                                   return_history=True)
+    finally:
+        torch.rand = orig_rand
+        ref_mod.GreensDistribution2D, ref_mod.ScreenedGreensDistribution2D = oG, oS
+    vals, steps, finals = [], [], []
+    for pi in range(len(points)):
+        for wk in hist[pi]:
+            vals.append(sum(c["contribution"] for c in wk["contributions"]))
+            steps.append(len(wk["path"]))
+            finals.append(wk["contributions"][-1]["point"].detach().numpy())
+    res = dict(points=points, n_walks=np.int64(n_walks), max_steps=np.int64(max_steps), eps=np.float32(eps),
+               seed=np.uint64(seed), walk_values=np.array(vals, np.float64), walk_steps=np.array(steps, np.int64),
+               final_points=np.array(finals, np.float32), u=u.detach().numpy().astype(np.float32).ravel(), nodes=nodes,
+               dirichlet=solver.dirichletBoundary.points.numpy().astype(np.float32))
+    if solver.neumannBoundary is not None:
+        res["neumann"] = solver.neumannBoundary.points.numpy().astype(np.float32)
+    if solver.use_delta_tracking:
+        res["sigma_bar"] = np.float64(solver.sigma_bar)
+    return res
+
+
+REPLAYS = {
+    # name: (points, walks, maxSteps, eps, seed)
+    "laplace_square": lambda: (S.laplace_square().points[:8], 64, 1000, 1e-4, 1234),
+    "manufactured_polynomial": lambda: (S.manufactured_polynomial().points[:4], 32, 800, 1e-4, 42),
+    "poisson_square": lambda: (S.poisson_square().points[:8], 64, 500, 1e-4, 7),
+    "variable_coefficients": lambda: (S.variable_coefficients().points[:4], 32, 1000, 1e-4, 99),
+    # electrodes next to the +-10 m current sources (x = -10.5, -7.5, 7.5, 10.5)
+    "dcr_dipole": lambda: (S.dcr_dipole().points[[20, 21, 26, 27]], 16, 500, 0.9, 2024),
+    "notebook_dcr": lambda: (S.notebook_dcr().points[[4, 5, 15, 16]], 8, 500, 0.9, 5),
+}
+
+
+def gen_replays(names):
+    for name in names:
+        t0 = time.time()
+        pts, W, ms, eps, seed = REPLAYS[name]()
+        res = replay(name, np.ascontiguousarray(pts, np.float32), W, ms, eps, seed)
+        np.savez_compressed(os.path.join(OUT, f"replay_{name}.npz"), **res)
+        print(f"replay_{name}.npz", len(res["walk_values"]), "walks", int(res["walk_steps"].sum()), "steps",
+              f"{time.time() - t0:.1f}s")
+
+
+# ---------------------------------------------------------------------------
+# G6: statistics with the reference's own RNG
+# ---------------------------------------------------------------------------
+STATS = {
+    "laplace_square": lambda: (S.laplace_square().points[:32], 500, 1000, 1e-4),
+    "manufactured_polynomial": lambda: (S.manufactured_polynomial().points, 150, 800, 1e-4),
+    "poisson_square": lambda: (S.poisson_square().points[:16], 400, 500, 1e-4),
+    "variable_coefficients": lambda: (S.variable_coefficients().points[:8], 100, 1000, 1e-4),
+    "dcr_dipole": lambda: (S.dcr_dipole().points[14:34:2], 60, 500, 0.9),
+    "notebook_dcr": lambda: (S.notebook_dcr().points[2:19:2], 40, 500, 0.9),
+}
+
+
+def _stats_worker(args):
+    name, pidx, pts, W, ms, eps, seed = args
+    torch.set_num_threads(1)
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    spec = ref_scenarios()[name]()
+    solver = build_ref_solver(spec)
+    with _quiet(), contextlib.redirect_stderr(io.StringIO()):
+        u, hist = solver.solve(torch.from_numpy(pts), nWalks=W, maxSteps=ms, eps=eps, return_history=True)
+    rows = []
+    for i in range(len(pts)):
+        v = np.array([sum(c["contribution"] for c in wk["contributions"]) for wk in hist[i]], np.float64)
+        s = np.array([len(wk["path"]) for wk in hist[i]], np.float64)
+        rows.append((pidx[i], v.mean(), v.std(ddof=1) / math.sqrt(len(v)), s.mean(), float(u[i, 0].detach())))
+    return rows
+
+
+def gen_stats(names, workers):
+    import multiprocessing as mp
+
+    for name in names:
+        t0 = time.time()
+        pts, W, ms, eps = STATS[name]()
+        pts = np.ascontiguousarray(pts, np.float32)
+        jobs = []
+        for i in range(len(pts)):
+            jobs.append((name, [i], pts[i:i + 1], W, ms, eps, 1000 + i))
+        with mp.get_context("fork").Pool(workers) as pool:
+            rows = [r for chunk in pool.map(_stats_worker, jobs) for r in chunk]
+        rows.sort()
+        arr = np.array([r[1:] for r in rows], np.float64)
+        np.savez_compressed(os.path.join(OUT, f"stats_{name}.npz"), points=pts, n_walks=np.int64(W),
+                            max_steps=np.int64(ms), eps=np.float32(eps), mean=arr[:, 0], stderr=arr[:, 1],
+                            mean_steps=arr[:, 2], u_ref=arr[:, 3])
+        print(f"stats_{name}.npz", f"{time.time() - t0:.1f}s", "mean steps", arr[:, 2].mean())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="geometry,fields,greens,sampler,replay,stats")
+    ap.add_argument("--scenarios", default="")
+    ap.add_argument("--stats-workers", type=int, default=8)
+    a = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    parts = set(a.only.split(","))
+    torch.set_num_threads(1)
+    if "geometry" in parts:
+        gen_geometry()
+    if "fields" in parts:
+        gen_fields()
+    if "greens" in parts:
+        gen_greens()
+    if "sampler" in parts:
+        gen_sampler_draws()
+    names = a.scenarios.split(",") if a.scenarios else list(REPLAYS)
+    if "replay" in parts:
+        gen_replays(names)
+    if "stats" in parts:
+        gen_stats(names, a.stats_workers)
+
+
+if __name__ == "__main__":
+    main()
