@@ -12,7 +12,7 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uin
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libwost.so")
+LIB_PATH = os.environ.get("WOST_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libwost.so")
 
 WOST_OK = 0
 WOST_ERR_INVALID_ARG = -1

@@ -466,6 +466,8 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if (W <= 0) return fail(WOST_ERR_INVALID_ARG, "nWalks must be >= 1 (got %lld)", (long long)W);
     if (max_steps < 0) return fail(WOST_ERR_INVALID_ARG, "maxSteps must be >= 0");
     if (!(eps == eps)) return fail(WOST_ERR_INVALID_ARG, "eps is NaN");
+    if (n_points > 0 && W > (int64_t(1) << 53) / n_points)
+        return fail(WOST_ERR_INVALID_ARG, "n_points * nWalks must stay below 2^53 walks");
     const int64_t nbpp = (W + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
     const int64_t nb_total = n_points * nbpp;
     if (block_begin < 0 || block_end < block_begin || block_end > nb_total)
@@ -504,10 +506,11 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * 3)) != WOST_OK) return rc;
 
     int blocks_per_cu = 0;
-    HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), &blocks_per_cu));
+    HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
+                           &blocks_per_cu));
     if (blocks_per_cu < 1)
         return fail(WOST_ERR_UNSUPPORTED, "walk kernel does not fit on a CU (polylines too large for LDS: %zu bytes)",
-                    walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2)));
+                    walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points));
 
     WalkArgs a{};
     a.points = h->d_points;
@@ -524,6 +527,8 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     a.rmin = eps / 2.0f;
     a.key0 = (uint32_t)seed;
     a.key1 = (uint32_t)(seed >> 32);
+    a.n_points = (int32_t)std::min<int64_t>(n_points, INT32_MAX);
+    a.inv_walks_per_point = 1.0 / (double)W;
 
     std::vector<int64_t> begins;
     std::vector<float> ms_walk, ms_red;

@@ -16,8 +16,8 @@
 namespace wost {
 
 constexpr float kPiF = 3.14159265358979323846f;
-constexpr int kChebA = 24;   // i0e on [0,8], t = x/4 - 1
-constexpr int kChebB = 20;   // sqrt(x) i0e(x) on (8,inf), t = 16/x - 1
+constexpr int kChebA = 17;   // i0e on [0,8], t = x/4 - 1           (max rel. error 5e-7 in float)
+constexpr int kChebB = 8;    // sqrt(x) i0e(x) on (8,inf), t = 16/x - 1 (max rel. error 2e-7 in float)
 
 // ---------------------------------------------------------------------------
 // Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11), the bijection of
@@ -99,8 +99,33 @@ WOST_HD Jet jet_mul(const Jet& a, const Jet& b) {
     return r;
 }
 
+// ---------------------------------------------------------------------------
+// Arithmetic of the coefficient fields, the Green's norm and the walk
+// direction. On the device these use the hardware transcendental / reciprocal
+// / square-root instructions (v_exp_f32, v_rcp_f32, v_sqrt_f32, v_sin_f32,
+// v_cos_f32: a few ulp) instead of the correctly rounded library sequences.
+// They feed values (contributions, weights), not the walk's geometric branch
+// decisions, which stay IEEE (see the polyline queries below). The host build
+// (sigma_bar grid) uses the C library.
+// ---------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+WOST_HD float f_exp(float x) { return __expf(x); }
+WOST_HD float f_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+WOST_HD float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+WOST_HD float f_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+WOST_HD float f_sin(float x) { return __sinf(x); }
+WOST_HD float f_cos(float x) { return __cosf(x); }
+#else
+WOST_HD float f_exp(float x) { return expf(x); }
+WOST_HD float f_rcp(float x) { return 1.0f / x; }
+WOST_HD float f_div(float a, float b) { return a / b; }
+WOST_HD float f_sqrt(float x) { return sqrtf(x); }
+WOST_HD float f_sin(float x) { return sinf(x); }
+WOST_HD float f_cos(float x) { return cosf(x); }
+#endif
+
 // torch.sigmoid in float32
-WOST_HD float sigmoidf(float z) { return 1.0f / (1.0f + expf(-z)); }
+WOST_HD float sigmoidf(float z) { return f_rcp(1.0f + f_exp(-z)); }
 
 WOST_HD float ipowf(float x, int n) {
     float r = 1.0f;
@@ -116,18 +141,18 @@ WOST_HD float factor_value(const DFactor& f, float x, float y) {
     case WOST_FK_EXP_QUAD: {
         float dx = x - p[0], dy = y - p[1];
         float q = p[2] * (dx * dx) + p[3] * (dy * dy) + p[4] * (dx * dy) + p[5] * dx + p[6] * dy + p[7];
-        return expf(q);
+        return f_exp(q);
     }
     case WOST_FK_SIN_LIN:
-        return sinf(p[0] * x + p[1] * y + p[2]);
+        return f_sin(p[0] * x + p[1] * y + p[2]);
     case WOST_FK_COS_LIN:
-        return cosf(p[0] * x + p[1] * y + p[2]);
+        return f_cos(p[0] * x + p[1] * y + p[2]);
     case WOST_FK_SIGMOID_LIN:
         return sigmoidf(p[0] * x + p[1] * y + p[2]);
     case WOST_FK_SIGMOID_RADIAL: {
         // utils.py:128-129: sdf = ||x - c|| - R ; sigmoid(k * sdf)
         float dx = x - p[1], dy = y - p[2];
-        float d = sqrtf(dx * dx + dy * dy);
+        float d = f_sqrt(dx * dx + dy * dy);
         return sigmoidf(p[0] * (d - p[3]));
     }
     case WOST_FK_IND_BOX:
@@ -162,7 +187,7 @@ WOST_HD Jet factor_jet(const DFactor& f, float x, float y) {
     case WOST_FK_EXP_QUAD: {
         float dx = x - p[0], dy = y - p[1];
         float q = p[2] * (dx * dx) + p[3] * (dy * dy) + p[4] * (dx * dy) + p[5] * dx + p[6] * dy + p[7];
-        float e = expf(q);
+        float e = f_exp(q);
         float qx = 2.f * p[2] * dx + p[4] * dy + p[5];
         float qy = 2.f * p[3] * dy + p[4] * dx + p[6];
         j.v = e;
@@ -174,7 +199,7 @@ WOST_HD Jet factor_jet(const DFactor& f, float x, float y) {
     case WOST_FK_SIN_LIN:
     case WOST_FK_COS_LIN: {
         float l = p[0] * x + p[1] * y + p[2];
-        float s = sinf(l), c = cosf(l);
+        float s = f_sin(l), c = f_cos(l);
         float aa = p[0] * p[0] + p[1] * p[1];
         if (f.kind == WOST_FK_SIN_LIN) {
             j.v = s; j.gx = c * p[0]; j.gy = c * p[1]; j.lap = -s * aa;
@@ -193,12 +218,12 @@ WOST_HD Jet factor_jet(const DFactor& f, float x, float y) {
     }
     case WOST_FK_SIGMOID_RADIAL: {
         float dx = x - p[1], dy = y - p[2];
-        float d = sqrtf(dx * dx + dy * dy);
+        float d = f_sqrt(dx * dx + dy * dy);
         float k = p[0];
         float s = sigmoidf(k * (d - p[3]));
         float s1 = s * (1.f - s);          // ds/dz
         float s2 = s1 * (1.f - 2.f * s);   // d2s/dz2
-        float inv = 1.f / d;
+        float inv = f_rcp(d);
         // z = k (d - R): grad z = k (x-c)/d, lap z = k/d (2-D), |grad z|^2 = k^2
         j.v = s;
         j.gx = s1 * k * dx * inv;
@@ -257,15 +282,15 @@ WOST_HD Jet field_jet(const DField& fd, TP terms, FP factors, float x, float y) 
 // back to sigma/alpha_c (:123-127, quirk Q9).
 WOST_HD float sigma_prime_from(const Jet& alpha, float sigma, bool detached) {
     float ac = alpha.v < 1e-8f ? 1e-8f : alpha.v;
-    float ratio = sigma / ac;
+    float ratio = f_div(sigma, ac);
     if (detached) return ratio;
     bool clamped = !(alpha.v >= 1e-8f);
     float gx = clamped ? 0.f : alpha.gx, gy = clamped ? 0.f : alpha.gy;
     float lap = 1e-8f + (clamped ? 0.f : alpha.lap);
-    float den = ac + 1e-8f;
-    float lx = gx / den, ly = gy / den;
+    float rden = f_rcp(ac + 1e-8f);
+    float lx = gx * rden, ly = gy * rden;
     float gn = lx * lx + ly * ly;
-    return ratio + 0.5f * (lap / ac - gn / 2.0f);
+    return ratio + 0.5f * (f_div(lap, ac) - gn / 2.0f);
 }
 
 // ---------------------------------------------------------------------------
@@ -291,9 +316,9 @@ WOST_HD float inv_i0(CP ca, CP cb, float x) {
     if (x <= 8.0f) {
         i0e = cheb_eval(ca, kChebA, x * 0.25f - 1.0f);
     } else {
-        i0e = cheb_eval(cb, kChebB, 16.0f / x - 1.0f) / sqrtf(x);
+        i0e = cheb_eval(cb, kChebB, 16.0f * f_rcp(x) - 1.0f) * f_rcp(f_sqrt(x));
     }
-    return expf(-x) / i0e;
+    return f_exp(-x) * f_rcp(i0e);
 }
 
 // ---------------------------------------------------------------------------
@@ -305,6 +330,7 @@ WOST_HD float inv_i0(CP ca, CP cb, float x) {
 // ---------------------------------------------------------------------------
 template <class TabP>
 WOST_HD float sample_rho(TabP tab, float u) {
+#pragma clang fp contract(off)
     float pos = u * (float)(WOST_SAMPLER_TABLE_N - 1);
     int i = (int)pos;
     if (i > WOST_SAMPLER_TABLE_N - 2) i = WOST_SAMPLER_TABLE_N - 2;
@@ -316,6 +342,8 @@ WOST_HD float sample_rho(TabP tab, float u) {
 // ---------------------------------------------------------------------------
 // Polyline queries (geometry/PolylinesSimple.py). VP is a pointer type to
 // float2 vertices (LDS or constant address space); the loops are wave-uniform.
+// Their branch decisions (clamps, silhouette signs, ray validity) must round
+// op by op like the reference's torch CPU ops, so FMA contraction is off here.
 // ---------------------------------------------------------------------------
 
 // distance_to_polyline_jit (:25-49): min over segments of the distance to the
@@ -323,6 +351,7 @@ WOST_HD float sample_rho(TabP tab, float u) {
 // propagates. sqrt is monotonic, so min(sqrt) == sqrt(min) bit for bit.
 template <class VP>
 WOST_HD float poly_distance(VP v, int nv, float px, float py) {
+#pragma clang fp contract(off)
     float best = INFINITY;
     bool nan = false;
     float2 a = v[0];
@@ -348,6 +377,7 @@ WOST_HD float poly_distance(VP v, int nv, float px, float py) {
 
 // is_silhouette_jit (:51-81) for interior vertex j in [1, nv-2].
 WOST_HD bool is_silhouette(float2 a, float2 b, float2 c, float px, float py) {
+#pragma clang fp contract(off)
     float abx = b.x - a.x, aby = b.y - a.y;
     float bcx = c.x - b.x, bcy = c.y - b.y;
     float apx = px - a.x, apy = py - a.y;
@@ -361,6 +391,7 @@ WOST_HD bool is_silhouette(float2 a, float2 b, float2 c, float px, float py) {
 // first and last vertex are never tested (quirk Q6).
 template <class VP>
 WOST_HD float silhouette_distance(VP v, int nv, float px, float py) {
+#pragma clang fp contract(off)
     float best = INFINITY;
     if (nv < 3) return best;
     float2 a = v[0], b = v[1];
@@ -380,6 +411,7 @@ WOST_HD float silhouette_distance(VP v, int nv, float px, float py) {
 // ray_intersection_jit (:104-132) for one segment: returns the SEGMENT
 // parameter s as the "time" (quirk Q1), +inf when invalid.
 WOST_HD float ray_segment_time(float2 a, float2 b, float qx, float qy, float dx, float dy) {
+#pragma clang fp contract(off)
     float ux = b.x - a.x, uy = b.y - a.y;
     float wx = qx - a.x, wy = qy - a.y;
     float den = dx * uy - dy * ux;
@@ -389,11 +421,35 @@ WOST_HD float ray_segment_time(float2 a, float2 b, float qx, float qy, float dx,
     return valid ? s : INFINITY;
 }
 
+// The same test with the two IEEE divisions done only for candidate segments.
+// The candidate filter uses the hardware reciprocal and is a strict superset
+// of the reference's validity (slack 1e-6 on s >= 0 / s <= 1, t >= 0), and the
+// candidates are then decided with the exact divisions, so the result is bit
+// for bit that of ray_segment_time.
+WOST_HD float ray_segment_time_filtered(float2 a, float2 b, float qx, float qy, float dx, float dy) {
+#pragma clang fp contract(off)
+    float ux = b.x - a.x, uy = b.y - a.y;
+    float wx = qx - a.x, wy = qy - a.y;
+    float den = dx * uy - dy * ux;
+    float ns = dx * wy - dy * wx;
+    float nt = ux * wy - uy * wx;
+    float rd = f_rcp(den);
+    float sa = ns * rd, ta = nt * rd;
+    float res = INFINITY;
+    if (sa >= -1e-6f && sa <= 1.000001f && ta >= 0.0f) {
+        float s = ns / den;
+        float t = nt / den;
+        if ((s >= 0.0f) && (s <= 1.0f) && (t > 0.0f)) res = s;
+    }
+    return res;
+}
+
 struct Hit { float x, y, nx, ny; bool hit; };
 
 // intersect_polylines_jit (:134-197).
 template <class VP>
 WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, float dyi, float r) {
+#pragma clang fp contract(off)
     Hit h;
     float dn = sqrtf(dxi * dxi + dyi * dyi);
     if (dn < 1e-10f) {
@@ -407,7 +463,7 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
     float2 a = v[0];
     for (int i = 1; i < nv; ++i) {
         float2 b = v[i];
-        float s = ray_segment_time(a, b, qx, qy, dx, dy);
+        float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
         if (s < best) { best = s; bi = i - 1; }   // first argmin (:177-178)
         a = b;
     }

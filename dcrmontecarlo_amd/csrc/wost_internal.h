@@ -26,7 +26,11 @@ struct WalkArgs {
     float rmin;                  // eps / 2 (solvers/WoStSolver.py:167)
     uint32_t key0, key1;         // Philox key = seed
     int32_t chunk;               // walks claimed per work-queue dequeue
+    int32_t n_points;            // query points (staged in LDS when <= kLdsPointsMax)
+    double inv_walks_per_point;  // 1/W for the point index of a walk id
 };
+
+constexpr int kLdsPointsMax = 1024;
 
 enum WalkMode : int {
     MODE_DIRICHLET = 0,      // Laplace, Dirichlet only
@@ -37,8 +41,8 @@ enum WalkMode : int {
     MODE_MIXED_DELTA = 5     // delta tracking + Neumann
 };
 
-size_t walk_lds_bytes(int mode, int nd, int nn);
-hipError_t walk_occupancy(int mode, int nd, int nn, int* blocks_per_cu);
+size_t walk_lds_bytes(int mode, int nd, int nn, int n_points);
+hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu);
 hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s);
 
 // Per-block reduction: block b covers local walks [begin[b], begin[b+1]).

@@ -85,33 +85,45 @@ struct ProgView {
 
 constexpr size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
-size_t walk_lds_bytes(int mode, int nd, int nn) {
+size_t walk_lds_bytes(int mode, int nd, int nn, int n_points) {
     bool neu = mode == MODE_MIXED || mode == MODE_MIXED_POISSON || mode == MODE_MIXED_DELTA;
     bool src = mode == MODE_POISSON || mode == MODE_MIXED_POISSON || mode == MODE_DELTA ||
                mode == MODE_MIXED_DELTA;
     size_t b = align16(sizeof(float2) * (size_t)nd);
     if (neu) b += align16(sizeof(float2) * (size_t)nn);
     if (src) b += align16(sizeof(float) * WOST_SAMPLER_TABLE_N);
+    if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
     return b;
 }
 
 // One walk-step of _solveUnified (solvers/WoStSolver.py:206-291) for every
 // active lane, with the finish/refill logic of loops 1-2 (:182-188, :294-311)
 // around it.
+#ifndef WOST_WALK_MIN_WAVES
+#define WOST_WALK_MIN_WAVES 6   // 6 waves/SIMD: measured best (tools/ab_bench.sh)
+#endif
 template <bool NEU, bool SRC, bool DELTA>
-__global__ void __launch_bounds__(kWalkBlock)
+__global__ void __launch_bounds__(kWalkBlock, WOST_WALK_MIN_WAVES)
 wost_walk_kernel(const WalkArgs A) {
+    // the walk's position updates round op by op like the reference (torch CPU
+    // has no FMA contraction); the field math it calls keeps FMAs
+#pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float2* sD = reinterpret_cast<float2*>(smem);
     float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
     float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
                                          (NEU ? align16(sizeof(float2) * (size_t)A.nn) : 0));
+    float2* sP = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(sT) +
+                                           (SRC ? align16(sizeof(float) * WOST_SAMPLER_TABLE_N) : 0));
+    const bool points_in_lds = A.n_points <= kLdsPointsMax;
 
     for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
     if (NEU)
         for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
     if (SRC)
         for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
+    if (points_in_lds)
+        for (int i = threadIdx.x; i < A.n_points; i += blockDim.x) sP[i] = A.points[i];
     __syncthreads();
 
     const ProgView P(A.prog);
@@ -179,8 +191,15 @@ wost_walk_kernel(const WalkArgs A) {
             const uint32_t rank = (uint32_t)__popcll(need & lanes_below);
             if ((need & lanebit) && rank < take) {
                 wid = (uint64_t)A.wid_begin + c_next + rank;
-                const uint64_t pid = wid / (uint64_t)A.walks_per_point;
-                const float2 q = A.points[pid];
+                // pid = wid / W without a 64-bit integer division: a double
+                // estimate (exact operands below 2^53) and one correction
+                uint64_t pid = (uint64_t)((double)wid * A.inv_walks_per_point);
+                const int64_t rem = (int64_t)(wid - pid * (uint64_t)A.walks_per_point);
+                if (rem < 0) --pid;
+                else if (rem >= A.walks_per_point) ++pid;
+                float2 q;
+                if (points_in_lds) q = sP[pid];
+                else q = A.points[pid];
                 px = q.x; py = q.y;
                 k = 0; dD = 1.0f; onB = false; nx = 0.f; ny = 1.f; w = 1.f; total = 0.f;
                 if (DELTA) ax = P.value(fA, px, py);
@@ -209,8 +228,7 @@ wost_walk_kernel(const WalkArgs A) {
                                     A.key0, A.key1);
         float theta = (u01(rn.x) * 2.0f) * kPiF;                     // :226
         if (NEU && onB) theta = theta / 2.0f + atan2f(ny, nx);       // :227-228 (quirk Q2)
-        float sn, cs;
-        sincosf(theta, &sn, &cs);                                    // :230-232
+        const float cs = f_cos(theta), sn = f_sin(theta);            // :230-232
 
         float xnx, xny;
         if (NEU) {                                                   // :235-236
@@ -241,7 +259,7 @@ wost_walk_kernel(const WalkArgs A) {
             if (!clipped) {
                 const float f = P.value(fF, yx, yy);
                 if (DELTA)
-                    c = ((f * gnorm) / sqrtf(aj.v * ax)) * w;        // :253-254
+                    c = (f * gnorm) * f_rcp(f_sqrt(aj.v * ax)) * w;  // :253-254
                 else
                     c = f * ((r * r) / 4.0f);                        // :256, utils.py:61
             }
@@ -252,14 +270,14 @@ wost_walk_kernel(const WalkArgs A) {
             const float mu = u01(rn.z);
             if (mu > sigma_bar * gnorm) {
                 const float an = clipped ? aj.v : P.value(fA, xnx, xny);
-                w = w * sqrtf(an / ax);                              // :277
+                w = w * f_sqrt(f_div(an, ax));                       // :277
                 px = xnx; py = xny; ax = an;
             } else {
                 const float sg = fS.present ? P.value(fS, yx, yy) : 0.0f;
                 const float spv = sigma_prime_from(aj, sg, detached);    // :281
-                float sc = 1.0f - spv / sigma_bar;
+                float sc = 1.0f - spv * inv_sb;
                 sc = (0.0f > sc) ? 0.0f : sc;                        // Python max(., 0.0) (:282)
-                w = (w * sqrtf(aj.v / ax)) * sc;                     // :283
+                w = (w * f_sqrt(f_div(aj.v, ax))) * sc;              // :283
                 px = yx; py = yy; ax = aj.v;
             }
         } else {
@@ -270,8 +288,8 @@ wost_walk_kernel(const WalkArgs A) {
     }
 }
 
-hipError_t walk_occupancy(int mode, int nd, int nn, int* blocks_per_cu) {
-    const size_t lds = walk_lds_bytes(mode, nd, nn);
+hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu) {
+    const size_t lds = walk_lds_bytes(mode, nd, nn, n_points);
     switch (mode) {
     case MODE_DIRICHLET:
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<false, false, false>, kWalkBlock, lds);
@@ -290,7 +308,7 @@ hipError_t walk_occupancy(int mode, int nd, int nn, int* blocks_per_cu) {
 }
 
 hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s) {
-    const size_t lds = walk_lds_bytes(mode, a.nd, a.nn);
+    const size_t lds = walk_lds_bytes(mode, a.nd, a.nn, a.n_points);
     switch (mode) {
     case MODE_DIRICHLET: wost_walk_kernel<false, false, false><<<grid, kWalkBlock, lds, s>>>(a); break;
     case MODE_POISSON: wost_walk_kernel<false, true, false><<<grid, kWalkBlock, lds, s>>>(a); break;

@@ -66,6 +66,7 @@ def _load():
     lib.orc_sigma_bar.restype = c_double
     lib.orc_sigma_bar.argtypes = [POINTER(OrcProblem)]
     lib.orc_philox.argtypes = [POINTER(c_uint32), c_uint32, c_uint32, POINTER(c_uint32)]
+    lib.orc_set_direction_perturbation.argtypes = [c_float]
     lib.orc_solve.restype = c_int32
     lib.orc_solve.argtypes = [POINTER(OrcProblem), fp, c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
                               c_uint64, c_int32, fp, POINTER(c_uint32)]
@@ -145,6 +146,10 @@ class Problem:
         s = s.astype(np.float64).reshape(-1, n_walks)
         se = v.std(axis=1, ddof=1) / np.sqrt(n_walks) if n_walks > 1 else np.zeros(v.shape[0])
         return v.mean(axis=1), se, s.mean(axis=1)
+
+
+def set_direction_perturbation(rel: float):
+    lib.orc_set_direction_perturbation(float(rel))
 
 
 def field_value(field, pts) -> np.ndarray:

@@ -41,6 +41,12 @@ void orc_philox(uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
 
 static float orc_u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
+/* Relative perturbation of the step direction (0 = off). Used only by the
+ * sensitivity test that measures how chaotic each scenario's walks are under
+ * an ulp-sized change (tests/test_oracle_golden.py). */
+static float orc_dir_perturb = 0.0f;
+void orc_set_direction_perturbation(float rel) { orc_dir_perturb = rel; }
+
 /* ------------------------------------------------------------------------ */
 /* Geometry: geometry/PolylinesSimple.py                                      */
 /* ------------------------------------------------------------------------ */
@@ -482,6 +488,7 @@ static void orc_walk(const orc_ctx* c, uint64_t wid, float x0, float y0, float* 
         float theta = (orc_u01(rn[0]) * 2.0f) * (float)ORC_PI;      /* :226 */
         if (onB && c->neu) theta = theta / 2.0f + atan2f(ny, nx);    /* :227-228 */
         float cs = cosf(theta), sn = sinf(theta);                    /* :230-232 */
+        if (orc_dir_perturb != 0.0f) { cs *= 1.0f + orc_dir_perturb; sn *= 1.0f - orc_dir_perturb; }
         float xnx, xny;
         if (c->neu) {                                                /* :236 */
             float o[5];

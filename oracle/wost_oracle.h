@@ -68,6 +68,9 @@ float orc_field_value(const orc_field* f, float x, float y);
 float orc_sigma_prime(const orc_problem* pb, float x, float y);
 double orc_sigma_bar(const orc_problem* pb);
 
+/* sensitivity probe: relative perturbation of the step direction (0 = off) */
+void orc_set_direction_perturbation(float rel);
+
 /* Philox4x32-10 */
 void orc_philox(uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]);
 

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Walk-steps/s of every scenario kernel variant on one GPU (device time of the walk
+kernel from libwost's HIP events, plus wall time of the solve). Honours WOST_LIB.
+Usage: python tools/scenario_bench.py [--scale 1.0] [--only a,b]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dcrmontecarlo_amd import perfmodel  # noqa: E402
+from dcrmontecarlo_amd import scenarios as S  # noqa: E402
+
+# (points, walks per point) sized for ~0.1-1 s per solve at ~1e10 steps/s
+SIZES = {
+    "laplace_square": (64, 200_000), "manufactured_polynomial": (16, 500_000), "poisson_square": (64, 200_000),
+    "variable_coefficients": (256, 20_000), "dcr_dipole": (48, 1_000_000), "notebook_dcr": (21, 200_000),
+    "wenner_topography": (256, 64),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    names = a.only.split(",") if a.only else list(SIZES)
+    out = {}
+    for name in names:
+        npts, W = SIZES[name]
+        W = max(1, int(W * a.scale))
+        sc = S.ALL[name]()
+        solver = sc.solver(device=int(os.environ.get("LOCAL_RANK", "0")))
+        pts = sc.points[:npts]
+        solver.solve(pts, nWalks=max(1, W // 10), maxSteps=sc.max_steps, eps=sc.eps, seed=1)   # warm-up
+        best = None
+        for r in range(a.reps):
+            t0 = time.perf_counter()
+            u, st = solver.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=100 + r, return_stats=True)
+            wall = time.perf_counter() - t0
+            t = solver.last_timing
+            rec = {"steps": int(t["total_steps"]), "kernel_ms": t["walk_kernel_ms"], "wall_s": wall,
+                   "grid": t["grid_blocks"]}
+            if best is None or rec["kernel_ms"] < best["kernel_ms"]:
+                best = rec
+        fps = perfmodel.flops_per_step(sc)
+        best["steps_per_s_kernel"] = best["steps"] / (best["kernel_ms"] * 1e-3)
+        best["steps_per_s_wall"] = best["steps"] / best["wall_s"]
+        best["model_tflops"] = fps * best["steps_per_s_kernel"] / 1e12
+        best["frac_fp32"] = best["model_tflops"] / perfmodel.FP32_PEAK_TFLOPS
+        best["mean_steps"] = best["steps"] / (npts * W)
+        best["config"] = f"{npts} pts x {W} walks"
+        out[name] = best
+        print(f"{name:26s} {best['config']:22s} {best['steps_per_s_kernel']:.3e} steps/s (kernel) "
+              f"{best['steps_per_s_wall']:.3e} (wall) {best['model_tflops']:.1f} TF ({100*best['frac_fp32']:.1f}%) "
+              f"grid {best['grid']} mean steps {best['mean_steps']:.1f}", flush=True)
+    print("JSON " + json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
