@@ -9,12 +9,14 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
 
 #include "wost_device.h"
 #include "wost_internal.h"
+#include "wost_jit.h"
 #include "wost_tables.h"
 
 using namespace wost;
@@ -153,6 +155,14 @@ struct wost_handle {
     std::vector<float> table;   // sampler nodes (built on first use)
     bool table_ready = false;
     bool prog_dirty = true;
+    uint64_t prog_version = 0;  // bumped whenever the program is rebuilt
+
+    // field-specialised walk kernel (wost_jit.cpp)
+    bool jit_enabled = true;
+    hipFunction_t jit_fn = nullptr;
+    int jit_mode = -1;
+    uint64_t jit_version = ~0ull;
+    std::string jit_error;
 
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
@@ -189,7 +199,29 @@ int upload_program(wost_handle* h) {
     }
     HIP_TRY(hipMemcpy(h->d_prog, h->prog.bytes.data(), h->prog.bytes.size(), hipMemcpyHostToDevice));
     h->prog_dirty = false;
+    ++h->prog_version;
     return WOST_OK;
+}
+
+// The field-specialised kernel for `mode`, or nullptr when it is disabled or
+// could not be built (the precompiled kernel is used then; same results).
+hipFunction_t jit_kernel(wost_handle* h, int mode) {
+    if (!h->jit_enabled) return nullptr;
+    if (h->jit_mode == mode && h->jit_version == h->prog_version) return h->jit_fn;
+    h->jit_fn = nullptr;
+    h->jit_mode = mode;
+    h->jit_version = h->prog_version;
+    const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors());
+    std::string err;
+    hipFunction_t fn = nullptr;
+    if (!jit_get_kernel(h->device, src, &fn, &err)) {
+        h->jit_error = err;
+        std::fprintf(stderr, "libwost: field-specialised kernel unavailable, using the precompiled one: %s\n",
+                     err.c_str());
+        return nullptr;
+    }
+    h->jit_fn = fn;
+    return fn;
 }
 
 int ensure_table(wost_handle* h) {
@@ -350,6 +382,7 @@ int wost_create(const wost_problem* pb, wost_handle** out) {
         return rc;
     }
     h->compat = pb->compat;
+    if (const char* e = std::getenv("WOST_JIT")) h->jit_enabled = std::strcmp(e, "0") != 0;
     // solvers/WoStSolver.py:54-64: any of sigma/alpha turns on delta tracking,
     // the missing one defaults to sigma = 0 / alpha = 1 (constant => Q9 fallback).
     h->delta = h->fields[SLOT_SIGMA].present || h->fields[SLOT_ALPHA].present;
@@ -505,9 +538,14 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, kMaxBatchWalks))) != WOST_OK) return rc;
     if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * 3)) != WOST_OK) return rc;
 
+    const hipFunction_t jfn = jit_kernel(h, mode);
+    const size_t lds = walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points);
     int blocks_per_cu = 0;
-    HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
-                           &blocks_per_cu));
+    if (jfn)
+        HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, kWalkBlock, lds));
+    else
+        HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
+                               &blocks_per_cu));
     if (blocks_per_cu < 1)
         return fail(WOST_ERR_UNSUPPORTED, "walk kernel does not fit on a CU (polylines too large for LDS: %zu bytes)",
                     walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points));
@@ -567,7 +605,12 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         h->timing.grid_blocks = grid;
 
         HIP_TRY(hipEventRecord(h->ev[0], h->stream));
-        HIP_TRY(launch_walk(mode, a, grid, h->stream));
+        if (jfn) {
+            void* args[] = {&a};
+            HIP_TRY(hipModuleLaunchKernel(jfn, grid, 1, 1, kWalkBlock, 1, 1, (unsigned)lds, h->stream, args, nullptr));
+        } else {
+            HIP_TRY(launch_walk(mode, a, grid, h->stream));
+        }
         HIP_TRY(hipEventRecord(h->ev[1], h->stream));
         HIP_TRY(launch_block_reduce(h->d_val, h->d_steps, h->d_begin, nb, h->d_bstats + 3 * (j - block_begin), h->stream));
         HIP_TRY(hipEventRecord(h->ev[2], h->stream));
@@ -609,6 +652,15 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     h->timing.n_launches = launches;
     h->timing.total_steps = steps_sum;
     h->timing.total_walks = (uint64_t)walks_total;
+    h->timing.jit = jfn ? 1 : 0;
+    return WOST_OK;
+}
+
+int wost_set_jit(wost_handle* h, int32_t enable) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    h->jit_enabled = enable != 0;
+    h->jit_fn = nullptr;
+    h->jit_mode = -1;
     return WOST_OK;
 }
 

@@ -1,17 +1,27 @@
 // wost_device.h -- arithmetic of one walk-step, shared by the gfx950 kernels
-// and by libwost's host-side setup (sigma_bar grid, table checks).
+// (precompiled and hiprtc-specialised) and by libwost's host-side setup
+// (sigma_bar grid).
 //
 // Everything here restates a piece of the reference's hot path; each function
 // cites the reference lines it follows. The arithmetic is float32 like the
 // reference's tensors (geometry/PolylinesSimple.py, solvers/WoStSolver.py).
 #pragma once
 
+#if !defined(__HIPCC_RTC__)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#endif
 #include "wost.h"
 
+// FMA contraction only within a single expression: the interpreted and the
+// hiprtc-specialised kernels then fuse the same multiply-adds and produce the
+// same bits. (The walk's geometric code turns contraction off entirely.)
+#pragma clang fp contract(on)
+
 #define WOST_HD __host__ __device__ __forceinline__
+#define WOST_INF __builtin_inff()
+#define WOST_NAN __builtin_nanf("")
 
 namespace wost {
 
@@ -54,8 +64,37 @@ WOST_HD U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 WOST_HD float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
 // ---------------------------------------------------------------------------
-// Fields (include/wost.h, "Coefficient fields"). Device layout of one field:
-// header + terms + factors inside one program buffer.
+// Arithmetic of the coefficient fields, the Green's norm and the walk
+// direction. On the device these use the hardware transcendental / reciprocal
+// / square-root instructions (v_exp_f32, v_rcp_f32, v_sqrt_f32, v_sin_f32,
+// v_cos_f32: a few ulp) instead of the correctly rounded library sequences.
+// They feed values (contributions, weights), not the walk's geometric branch
+// decisions, which stay IEEE (see the polyline queries below). The host build
+// (sigma_bar grid) uses the C library.
+// ---------------------------------------------------------------------------
+#if defined(__HIP_DEVICE_COMPILE__)
+WOST_HD float f_exp(float x) { return __expf(x); }
+WOST_HD float f_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+WOST_HD float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+WOST_HD float f_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+WOST_HD float f_sin(float x) { return __sinf(x); }
+WOST_HD float f_cos(float x) { return __cosf(x); }
+#else
+WOST_HD float f_exp(float x) { return expf(x); }
+WOST_HD float f_rcp(float x) { return 1.0f / x; }
+WOST_HD float f_div(float a, float b) { return a / b; }
+WOST_HD float f_sqrt(float x) { return sqrtf(x); }
+WOST_HD float f_sin(float x) { return sinf(x); }
+WOST_HD float f_cos(float x) { return cosf(x); }
+#endif
+
+// ---------------------------------------------------------------------------
+// Fields (include/wost.h, "Coefficient fields"). A field is
+//     sum_t coef_t * prod_k factor_k(x, y)
+// evaluated left to right: prod = coef, prod *= factor_1, ...; acc += prod.
+// The interpreter (field_value / field_jet over a program buffer) and the
+// hiprtc-generated code (wost_jit.cpp) perform exactly this sequence of calls
+// to the per-kind functions below, so both give the same bits.
 // ---------------------------------------------------------------------------
 struct alignas(16) DFactor {
     int32_t kind;
@@ -90,6 +129,9 @@ struct alignas(16) DProgram {
 
 struct Jet { float v, gx, gy, lap; };
 
+WOST_HD Jet jet_const(float c) { return Jet{c, 0.f, 0.f, 0.f}; }
+WOST_HD Jet jet_scale(float c, const Jet& b) { return Jet{c * b.v, c * b.gx, c * b.gy, c * b.lap}; }
+WOST_HD Jet jet_add(const Jet& a, const Jet& b) { return Jet{a.v + b.v, a.gx + b.gx, a.gy + b.gy, a.lap + b.lap}; }
 WOST_HD Jet jet_mul(const Jet& a, const Jet& b) {
     Jet r;
     r.v = a.v * b.v;
@@ -98,31 +140,6 @@ WOST_HD Jet jet_mul(const Jet& a, const Jet& b) {
     r.lap = a.v * b.lap + b.v * a.lap + 2.0f * (a.gx * b.gx + a.gy * b.gy);
     return r;
 }
-
-// ---------------------------------------------------------------------------
-// Arithmetic of the coefficient fields, the Green's norm and the walk
-// direction. On the device these use the hardware transcendental / reciprocal
-// / square-root instructions (v_exp_f32, v_rcp_f32, v_sqrt_f32, v_sin_f32,
-// v_cos_f32: a few ulp) instead of the correctly rounded library sequences.
-// They feed values (contributions, weights), not the walk's geometric branch
-// decisions, which stay IEEE (see the polyline queries below). The host build
-// (sigma_bar grid) uses the C library.
-// ---------------------------------------------------------------------------
-#if defined(__HIP_DEVICE_COMPILE__)
-WOST_HD float f_exp(float x) { return __expf(x); }
-WOST_HD float f_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-WOST_HD float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
-WOST_HD float f_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-WOST_HD float f_sin(float x) { return __sinf(x); }
-WOST_HD float f_cos(float x) { return __cosf(x); }
-#else
-WOST_HD float f_exp(float x) { return expf(x); }
-WOST_HD float f_rcp(float x) { return 1.0f / x; }
-WOST_HD float f_div(float a, float b) { return a / b; }
-WOST_HD float f_sqrt(float x) { return sqrtf(x); }
-WOST_HD float f_sin(float x) { return sinf(x); }
-WOST_HD float f_cos(float x) { return cosf(x); }
-#endif
 
 // torch.sigmoid in float32
 WOST_HD float sigmoidf(float z) { return f_rcp(1.0f + f_exp(-z)); }
@@ -133,116 +150,113 @@ WOST_HD float ipowf(float x, int n) {
     return r;
 }
 
+// ---- per-kind values ------------------------------------------------------
+WOST_HD float fv_mono(float x, float y, int a, int b) { return ipowf(x, a) * ipowf(y, b); }
+WOST_HD float fv_exp_quad(float x, float y, float cx, float cy, float axx, float ayy, float axy, float ax,
+                          float ay, float a0) {
+    float dx = x - cx, dy = y - cy;
+    return f_exp(axx * (dx * dx) + ayy * (dy * dy) + axy * (dx * dy) + ax * dx + ay * dy + a0);
+}
+WOST_HD float fv_sin_lin(float x, float y, float a, float b, float c) { return f_sin(a * x + b * y + c); }
+WOST_HD float fv_cos_lin(float x, float y, float a, float b, float c) { return f_cos(a * x + b * y + c); }
+WOST_HD float fv_sigmoid_lin(float x, float y, float a, float b, float c) { return sigmoidf(a * x + b * y + c); }
+// utils.py:128-129: sdf = ||x - c|| - R ; sigmoid(k * sdf)
+WOST_HD float fv_sigmoid_radial(float x, float y, float k, float cx, float cy, float R) {
+    float dx = x - cx, dy = y - cy;
+    return sigmoidf(k * (f_sqrt(dx * dx + dy * dy) - R));
+}
+WOST_HD float fv_ind_box(float x, float y, float x0, float x1, float y0, float y1) {
+    return (x >= x0 && x <= x1 && y >= y0 && y <= y1) ? 1.0f : 0.0f;
+}
+WOST_HD float fv_ind_disk(float x, float y, float cx, float cy, float r2) {
+    float dx = x - cx, dy = y - cy;
+    return (dx * dx + dy * dy <= r2) ? 1.0f : 0.0f;
+}
+
+// ---- per-kind jets (value, gradient, Laplacian) ----------------------------
+WOST_HD Jet fj_mono(float x, float y, int a, int b) {
+    float xa2 = a >= 2 ? ipowf(x, a - 2) : 0.f;
+    float xa1 = a >= 1 ? (a >= 2 ? xa2 * x : 1.f) : 0.f;
+    float xa = a >= 1 ? xa1 * x : 1.f;
+    float yb2 = b >= 2 ? ipowf(y, b - 2) : 0.f;
+    float yb1 = b >= 1 ? (b >= 2 ? yb2 * y : 1.f) : 0.f;
+    float yb = b >= 1 ? yb1 * y : 1.f;
+    Jet j;
+    j.v = xa * yb;
+    j.gx = (float)a * xa1 * yb;
+    j.gy = (float)b * xa * yb1;
+    j.lap = (float)(a * (a - 1)) * xa2 * yb + (float)(b * (b - 1)) * xa * yb2;
+    return j;
+}
+WOST_HD Jet fj_exp_quad(float x, float y, float cx, float cy, float axx, float ayy, float axy, float ax, float ay,
+                        float a0) {
+    float dx = x - cx, dy = y - cy;
+    float e = f_exp(axx * (dx * dx) + ayy * (dy * dy) + axy * (dx * dy) + ax * dx + ay * dy + a0);
+    float qx = 2.f * axx * dx + axy * dy + ax;
+    float qy = 2.f * ayy * dy + axy * dx + ay;
+    return Jet{e, e * qx, e * qy, e * (qx * qx + qy * qy + 2.f * (axx + ayy))};
+}
+WOST_HD Jet fj_sin_lin(float x, float y, float a, float b, float c) {
+    float l = a * x + b * y + c, s = f_sin(l), co = f_cos(l);
+    return Jet{s, co * a, co * b, -s * (a * a + b * b)};
+}
+WOST_HD Jet fj_cos_lin(float x, float y, float a, float b, float c) {
+    float l = a * x + b * y + c, s = f_sin(l), co = f_cos(l);
+    return Jet{co, -s * a, -s * b, -co * (a * a + b * b)};
+}
+WOST_HD Jet fj_sigmoid_lin(float x, float y, float a, float b, float c) {
+    float s = sigmoidf(a * x + b * y + c);
+    float s1 = s * (1.f - s), s2 = s1 * (1.f - 2.f * s);
+    return Jet{s, s1 * a, s1 * b, s2 * (a * a + b * b)};
+}
+WOST_HD Jet fj_sigmoid_radial(float x, float y, float k, float cx, float cy, float R) {
+    float dx = x - cx, dy = y - cy;
+    float d = f_sqrt(dx * dx + dy * dy);
+    float s = sigmoidf(k * (d - R));
+    float s1 = s * (1.f - s);          // ds/dz
+    float s2 = s1 * (1.f - 2.f * s);   // d2s/dz2
+    float inv = f_rcp(d);
+    // z = k (d - R): grad z = k (x-c)/d, lap z = k/d (2-D), |grad z|^2 = k^2
+    return Jet{s, s1 * k * dx * inv, s1 * k * dy * inv, s2 * k * k + s1 * k * inv};
+}
+WOST_HD Jet fj_ind_box(float x, float y, float x0, float x1, float y0, float y1) {
+    return jet_const(fv_ind_box(x, y, x0, x1, y0, y1));
+}
+WOST_HD Jet fj_ind_disk(float x, float y, float cx, float cy, float r2) { return jet_const(fv_ind_disk(x, y, cx, cy, r2)); }
+
+// ---- dispatch over a program factor (interpreter) ---------------------------
 WOST_HD float factor_value(const DFactor& f, float x, float y) {
     const float* p = f.p;
     switch (f.kind) {
-    case WOST_FK_MONO:
-        return ipowf(x, (int)p[0]) * ipowf(y, (int)p[1]);
-    case WOST_FK_EXP_QUAD: {
-        float dx = x - p[0], dy = y - p[1];
-        float q = p[2] * (dx * dx) + p[3] * (dy * dy) + p[4] * (dx * dy) + p[5] * dx + p[6] * dy + p[7];
-        return f_exp(q);
-    }
-    case WOST_FK_SIN_LIN:
-        return f_sin(p[0] * x + p[1] * y + p[2]);
-    case WOST_FK_COS_LIN:
-        return f_cos(p[0] * x + p[1] * y + p[2]);
-    case WOST_FK_SIGMOID_LIN:
-        return sigmoidf(p[0] * x + p[1] * y + p[2]);
-    case WOST_FK_SIGMOID_RADIAL: {
-        // utils.py:128-129: sdf = ||x - c|| - R ; sigmoid(k * sdf)
-        float dx = x - p[1], dy = y - p[2];
-        float d = f_sqrt(dx * dx + dy * dy);
-        return sigmoidf(p[0] * (d - p[3]));
-    }
-    case WOST_FK_IND_BOX:
-        return (x >= p[0] && x <= p[1] && y >= p[2] && y <= p[3]) ? 1.0f : 0.0f;
-    case WOST_FK_IND_DISK: {
-        float dx = x - p[0], dy = y - p[1];
-        return (dx * dx + dy * dy <= p[2]) ? 1.0f : 0.0f;
-    }
-    default:
-        return NAN;
+    case WOST_FK_MONO: return fv_mono(x, y, (int)p[0], (int)p[1]);
+    case WOST_FK_EXP_QUAD: return fv_exp_quad(x, y, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
+    case WOST_FK_SIN_LIN: return fv_sin_lin(x, y, p[0], p[1], p[2]);
+    case WOST_FK_COS_LIN: return fv_cos_lin(x, y, p[0], p[1], p[2]);
+    case WOST_FK_SIGMOID_LIN: return fv_sigmoid_lin(x, y, p[0], p[1], p[2]);
+    case WOST_FK_SIGMOID_RADIAL: return fv_sigmoid_radial(x, y, p[0], p[1], p[2], p[3]);
+    case WOST_FK_IND_BOX: return fv_ind_box(x, y, p[0], p[1], p[2], p[3]);
+    case WOST_FK_IND_DISK: return fv_ind_disk(x, y, p[0], p[1], p[2]);
+    default: return WOST_NAN;
     }
 }
 
 WOST_HD Jet factor_jet(const DFactor& f, float x, float y) {
     const float* p = f.p;
-    Jet j{0.f, 0.f, 0.f, 0.f};
     switch (f.kind) {
-    case WOST_FK_MONO: {
-        int a = (int)p[0], b = (int)p[1];
-        float xa2 = a >= 2 ? ipowf(x, a - 2) : 0.f;
-        float xa1 = a >= 1 ? (a >= 2 ? xa2 * x : 1.f) : 0.f;
-        float xa = a >= 1 ? xa1 * x : 1.f;
-        float yb2 = b >= 2 ? ipowf(y, b - 2) : 0.f;
-        float yb1 = b >= 1 ? (b >= 2 ? yb2 * y : 1.f) : 0.f;
-        float yb = b >= 1 ? yb1 * y : 1.f;
-        j.v = xa * yb;
-        j.gx = (float)a * xa1 * yb;
-        j.gy = (float)b * xa * yb1;
-        j.lap = (float)(a * (a - 1)) * xa2 * yb + (float)(b * (b - 1)) * xa * yb2;
-        return j;
-    }
-    case WOST_FK_EXP_QUAD: {
-        float dx = x - p[0], dy = y - p[1];
-        float q = p[2] * (dx * dx) + p[3] * (dy * dy) + p[4] * (dx * dy) + p[5] * dx + p[6] * dy + p[7];
-        float e = f_exp(q);
-        float qx = 2.f * p[2] * dx + p[4] * dy + p[5];
-        float qy = 2.f * p[3] * dy + p[4] * dx + p[6];
-        j.v = e;
-        j.gx = e * qx;
-        j.gy = e * qy;
-        j.lap = e * (qx * qx + qy * qy + 2.f * (p[2] + p[3]));
-        return j;
-    }
-    case WOST_FK_SIN_LIN:
-    case WOST_FK_COS_LIN: {
-        float l = p[0] * x + p[1] * y + p[2];
-        float s = f_sin(l), c = f_cos(l);
-        float aa = p[0] * p[0] + p[1] * p[1];
-        if (f.kind == WOST_FK_SIN_LIN) {
-            j.v = s; j.gx = c * p[0]; j.gy = c * p[1]; j.lap = -s * aa;
-        } else {
-            j.v = c; j.gx = -s * p[0]; j.gy = -s * p[1]; j.lap = -c * aa;
-        }
-        return j;
-    }
-    case WOST_FK_SIGMOID_LIN: {
-        float s = sigmoidf(p[0] * x + p[1] * y + p[2]);
-        float s1 = s * (1.f - s);
-        float s2 = s1 * (1.f - 2.f * s);
-        j.v = s; j.gx = s1 * p[0]; j.gy = s1 * p[1];
-        j.lap = s2 * (p[0] * p[0] + p[1] * p[1]);
-        return j;
-    }
-    case WOST_FK_SIGMOID_RADIAL: {
-        float dx = x - p[1], dy = y - p[2];
-        float d = f_sqrt(dx * dx + dy * dy);
-        float k = p[0];
-        float s = sigmoidf(k * (d - p[3]));
-        float s1 = s * (1.f - s);          // ds/dz
-        float s2 = s1 * (1.f - 2.f * s);   // d2s/dz2
-        float inv = f_rcp(d);
-        // z = k (d - R): grad z = k (x-c)/d, lap z = k/d (2-D), |grad z|^2 = k^2
-        j.v = s;
-        j.gx = s1 * k * dx * inv;
-        j.gy = s1 * k * dy * inv;
-        j.lap = s2 * k * k + s1 * k * inv;
-        return j;
-    }
-    case WOST_FK_IND_BOX:
-    case WOST_FK_IND_DISK:
-        j.v = factor_value(f, x, y);
-        return j;
-    default:
-        j.v = NAN;
-        return j;
+    case WOST_FK_MONO: return fj_mono(x, y, (int)p[0], (int)p[1]);
+    case WOST_FK_EXP_QUAD: return fj_exp_quad(x, y, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
+    case WOST_FK_SIN_LIN: return fj_sin_lin(x, y, p[0], p[1], p[2]);
+    case WOST_FK_COS_LIN: return fj_cos_lin(x, y, p[0], p[1], p[2]);
+    case WOST_FK_SIGMOID_LIN: return fj_sigmoid_lin(x, y, p[0], p[1], p[2]);
+    case WOST_FK_SIGMOID_RADIAL: return fj_sigmoid_radial(x, y, p[0], p[1], p[2], p[3]);
+    case WOST_FK_IND_BOX: return fj_ind_box(x, y, p[0], p[1], p[2], p[3]);
+    case WOST_FK_IND_DISK: return fj_ind_disk(x, y, p[0], p[1], p[2]);
+    default: return Jet{WOST_NAN, 0.f, 0.f, 0.f};
     }
 }
 
 // Field evaluation. TP/FP are pointer types to DTerm/DFactor: plain pointers
-// on the host, constant-address-space pointers on the device so that the
+// on the host, constant-address-space views on the device so that the
 // wave-uniform reads become scalar (SMEM) loads.
 template <class TP, class FP>
 WOST_HD float field_value(const DField& fd, TP terms, FP factors, float x, float y) {
@@ -259,17 +273,21 @@ WOST_HD float field_value(const DField& fd, TP terms, FP factors, float x, float
     return acc;
 }
 
+// Term jets: constant term -> jet_const(c); otherwise jet_scale(c, first
+// factor) then jet_mul with the others.
 template <class TP, class FP>
 WOST_HD Jet field_jet(const DField& fd, TP terms, FP factors, float x, float y) {
-    Jet acc{0.f, 0.f, 0.f, 0.f};
+    Jet acc = jet_const(0.0f);
     for (int t = 0; t < fd.n_terms; ++t) {
         DTerm tm = terms[fd.first_term + t];
-        Jet prod{tm.coef, 0.f, 0.f, 0.f};
-        for (int k = 0; k < tm.nf; ++k) {
-            DFactor f = factors[tm.first + k];
-            prod = jet_mul(prod, factor_jet(f, x, y));
+        Jet prod;
+        if (tm.nf == 0) {
+            prod = jet_const(tm.coef);
+        } else {
+            prod = jet_scale(tm.coef, factor_jet(factors[tm.first], x, y));
+            for (int k = 1; k < tm.nf; ++k) prod = jet_mul(prod, factor_jet(factors[tm.first + k], x, y));
         }
-        acc.v += prod.v; acc.gx += prod.gx; acc.gy += prod.gy; acc.lap += prod.lap;
+        acc = jet_add(acc, prod);
     }
     return acc;
 }
@@ -297,7 +315,7 @@ WOST_HD float sigma_prime_from(const Jet& alpha, float sigma, bool detached) {
 // Screened Green's function norm (solvers/utils.py:29-44):
 //   G_norm(R) = (1/sigma_bar) (1 - 1/I0(R sqrt(sigma_bar)))
 // with 1/I0(x) = exp(-x) / i0e(x); i0e from Chebyshev series whose
-// coefficients the host fits in double precision (wost_api.hip).
+// coefficients the host fits in double precision (wost_tables.cpp).
 // ---------------------------------------------------------------------------
 template <class CP>
 WOST_HD float cheb_eval(CP c, int n, float t) {
@@ -352,7 +370,7 @@ WOST_HD float sample_rho(TabP tab, float u) {
 template <class VP>
 WOST_HD float poly_distance(VP v, int nv, float px, float py) {
 #pragma clang fp contract(off)
-    float best = INFINITY;
+    float best = WOST_INF;
     bool nan = false;
     float2 a = v[0];
     for (int i = 1; i < nv; ++i) {
@@ -372,7 +390,7 @@ WOST_HD float poly_distance(VP v, int nv, float px, float py) {
         best = d2 < best ? d2 : best;
         a = b;
     }
-    return nan ? NAN : sqrtf(best);
+    return nan ? WOST_NAN : sqrtf(best);
 }
 
 // is_silhouette_jit (:51-81) for interior vertex j in [1, nv-2].
@@ -392,7 +410,7 @@ WOST_HD bool is_silhouette(float2 a, float2 b, float2 c, float px, float py) {
 template <class VP>
 WOST_HD float silhouette_distance(VP v, int nv, float px, float py) {
 #pragma clang fp contract(off)
-    float best = INFINITY;
+    float best = WOST_INF;
     if (nv < 3) return best;
     float2 a = v[0], b = v[1];
     for (int j = 1; j + 1 < nv; ++j) {
@@ -405,7 +423,7 @@ WOST_HD float silhouette_distance(VP v, int nv, float px, float py) {
         a = b;
         b = c;
     }
-    return best == INFINITY ? best : sqrtf(best);
+    return best == WOST_INF ? best : sqrtf(best);
 }
 
 // ray_intersection_jit (:104-132) for one segment: returns the SEGMENT
@@ -418,7 +436,7 @@ WOST_HD float ray_segment_time(float2 a, float2 b, float qx, float qy, float dx,
     float s = (dx * wy - dy * wx) / den;
     float t = (ux * wy - uy * wx) / den;
     bool valid = (s >= 0.0f) && (s <= 1.0f) && (t > 0.0f);
-    return valid ? s : INFINITY;
+    return valid ? s : WOST_INF;
 }
 
 // The same test with the two IEEE divisions done only for candidate segments.
@@ -435,7 +453,7 @@ WOST_HD float ray_segment_time_filtered(float2 a, float2 b, float qx, float qy, 
     float nt = ux * wy - uy * wx;
     float rd = f_rcp(den);
     float sa = ns * rd, ta = nt * rd;
-    float res = INFINITY;
+    float res = WOST_INF;
     if (sa >= -1e-6f && sa <= 1.000001f && ta >= 0.0f) {
         float s = ns / den;
         float t = nt / den;
@@ -458,7 +476,7 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
     }
     float dx = dxi / dn, dy = dyi / dn;
     float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
-    float best = INFINITY;
+    float best = WOST_INF;
     int bi = -1;
     float2 a = v[0];
     for (int i = 1; i < nv; ++i) {

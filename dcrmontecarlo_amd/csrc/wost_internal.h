@@ -1,36 +1,14 @@
-// wost_internal.h -- launch interface between libwost's host code (wost_api.hip)
-// and its gfx950 kernels (wost_kernels.hip). Not part of the public ABI.
+// wost_internal.h -- launch interface between libwost's host code (wost_api.hip,
+// wost_jit.cpp) and its gfx950 kernels (wost_kernels.hip). Not part of the
+// public ABI.
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "wost_walk.h"
+
 namespace wost {
-
-// Arguments of the walk kernel, passed by value in the kernarg segment.
-struct WalkArgs {
-    const float2* points;        // [n_points] query points
-    const float2* dverts;        // Dirichlet polyline vertices
-    const float2* nverts;        // Neumann polyline vertices (may be null)
-    const float* table;          // sampler inverse-CDF nodes (may be null)
-    const char* prog;            // DProgram + terms + factors
-    float* out_val;              // [count] per-walk estimate
-    uint32_t* out_steps;         // [count] per-walk step count
-    unsigned long long* counter; // work-queue head (zeroed before launch)
-    int64_t wid_begin;           // global id of local walk 0
-    int64_t count;               // walks in this launch
-    int64_t walks_per_point;     // W: point of global walk g is g / W
-    int32_t nd, nn;              // vertex counts
-    int32_t max_steps;
-    float eps;
-    float rmin;                  // eps / 2 (solvers/WoStSolver.py:167)
-    uint32_t key0, key1;         // Philox key = seed
-    int32_t chunk;               // walks claimed per work-queue dequeue
-    int32_t n_points;            // query points (staged in LDS when <= kLdsPointsMax)
-    double inv_walks_per_point;  // 1/W for the point index of a walk id
-};
-
-constexpr int kLdsPointsMax = 1024;
 
 enum WalkMode : int {
     MODE_DIRICHLET = 0,      // Laplace, Dirichlet only
@@ -41,7 +19,15 @@ enum WalkMode : int {
     MODE_MIXED_DELTA = 5     // delta tracking + Neumann
 };
 
-size_t walk_lds_bytes(int mode, int nd, int nn, int n_points);
+inline bool mode_neu(int m) { return m == MODE_MIXED || m == MODE_MIXED_POISSON || m == MODE_MIXED_DELTA; }
+inline bool mode_src(int m) { return m == MODE_POISSON || m == MODE_MIXED_POISSON || m == MODE_DELTA || m == MODE_MIXED_DELTA; }
+inline bool mode_delta(int m) { return m == MODE_DELTA || m == MODE_MIXED_DELTA; }
+
+inline size_t walk_lds_bytes(int mode, int nd, int nn, int n_points) {
+    return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points);
+}
+
+// precompiled (interpreted-field) walk kernels
 hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu);
 hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s);
 
@@ -55,7 +41,5 @@ hipError_t launch_geometry_query(int op, const float2* verts, int nv, const floa
 
 hipError_t launch_eval_field(const char* prog, int which, const float2* pts, int64_t n,
                              float4* out, hipStream_t s);
-
-constexpr int kWalkBlock = 256;
 
 }  // namespace wost

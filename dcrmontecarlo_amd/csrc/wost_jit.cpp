@@ -1,0 +1,271 @@
+// wost_jit.cpp -- see wost_jit.h.
+#include "wost_jit.h"
+
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <vector>
+
+// Header sources embedded at build time (Makefile: wost_embedded.cpp).
+extern const char wost_embedded_wost_h[];
+extern const char wost_embedded_wost_device_h[];
+extern const char wost_embedded_wost_walk_h[];
+
+namespace wost {
+namespace {
+
+// Exact float32 literal (hex float), or a builtin for non-finite values.
+std::string lit(float v) {
+    if (v != v) return "__builtin_nanf(\"\")";
+    if (v == __builtin_inff()) return "__builtin_inff()";
+    if (v == -__builtin_inff()) return "(-__builtin_inff())";
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "%af", (double)v);
+    return buf;
+}
+
+std::string factor_call(const DFactor& f, bool jet) {
+    const float* p = f.p;
+    std::ostringstream o;
+    const char* pre = jet ? "wost::fj_" : "wost::fv_";
+    switch (f.kind) {
+    case WOST_FK_MONO:
+        o << pre << "mono(x, y, " << (int)p[0] << ", " << (int)p[1] << ")";
+        break;
+    case WOST_FK_EXP_QUAD:
+        o << pre << "exp_quad(x, y";
+        for (int k = 0; k < 8; ++k) o << ", " << lit(p[k]);
+        o << ")";
+        break;
+    case WOST_FK_SIN_LIN:
+        o << pre << "sin_lin(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ")";
+        break;
+    case WOST_FK_COS_LIN:
+        o << pre << "cos_lin(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ")";
+        break;
+    case WOST_FK_SIGMOID_LIN:
+        o << pre << "sigmoid_lin(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ")";
+        break;
+    case WOST_FK_SIGMOID_RADIAL:
+        o << pre << "sigmoid_radial(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ", "
+          << lit(p[3]) << ")";
+        break;
+    case WOST_FK_IND_BOX:
+        o << pre << "ind_box(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ", " << lit(p[3])
+          << ")";
+        break;
+    case WOST_FK_IND_DISK:
+        o << pre << "ind_disk(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ")";
+        break;
+    default:
+        o << (jet ? "wost::Jet{__builtin_nanf(\"\"), 0.f, 0.f, 0.f}" : "__builtin_nanf(\"\")");
+    }
+    return o.str();
+}
+
+// Same operation sequence as wost::field_value.
+std::string value_body(const DField& fd, const DTerm* terms, const DFactor* factors) {
+    std::ostringstream o;
+    o << "        float acc = 0.0f;\n";
+    for (int t = 0; t < fd.n_terms; ++t) {
+        const DTerm& tm = terms[fd.first_term + t];
+        o << "        { float t = " << lit(tm.coef) << ";";
+        for (int k = 0; k < tm.nf; ++k) o << " t = t * " << factor_call(factors[tm.first + k], false) << ";";
+        o << " acc = acc + t; }\n";
+    }
+    o << "        return acc;\n";
+    return o.str();
+}
+
+// Same operation sequence as wost::field_jet.
+std::string jet_body(const DField& fd, const DTerm* terms, const DFactor* factors) {
+    std::ostringstream o;
+    o << "        wost::Jet acc = wost::jet_const(0.0f);\n";
+    for (int t = 0; t < fd.n_terms; ++t) {
+        const DTerm& tm = terms[fd.first_term + t];
+        if (tm.nf == 0) {
+            o << "        acc = wost::jet_add(acc, wost::jet_const(" << lit(tm.coef) << "));\n";
+            continue;
+        }
+        o << "        { wost::Jet t = wost::jet_scale(" << lit(tm.coef) << ", " << factor_call(factors[tm.first], true)
+          << ");";
+        for (int k = 1; k < tm.nf; ++k) o << " t = wost::jet_mul(t, " << factor_call(factors[tm.first + k], true) << ");";
+        o << " acc = wost::jet_add(acc, t); }\n";
+    }
+    o << "        return acc;\n";
+    return o.str();
+}
+
+uint64_t fnv1a(const std::string& s) {
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+std::string cache_dir() {
+    if (const char* d = std::getenv("WOST_JIT_CACHE")) return d;
+    if (const char* x = std::getenv("XDG_CACHE_HOME")) return std::string(x) + "/wost";
+    if (const char* h = std::getenv("HOME")) return std::string(h) + "/.cache/wost";
+    return "";
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return !out.empty();
+}
+
+void write_file_atomic(const std::string& dir, const std::string& name, const std::vector<char>& data) {
+    if (dir.empty()) return;
+    std::string cur;
+    for (size_t i = 0; i <= dir.size(); ++i) {   // mkdir -p
+        if (i == dir.size() || dir[i] == '/') {
+            cur = dir.substr(0, i);
+            if (!cur.empty()) mkdir(cur.c_str(), 0755);
+        }
+    }
+    std::string tmp = dir + "/" + name + ".tmp." + std::to_string(getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return;
+        f.write(data.data(), (std::streamsize)data.size());
+        if (!f) return;
+    }
+    std::rename(tmp.c_str(), (dir + "/" + name).c_str());
+}
+
+struct Entry {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+};
+
+std::mutex g_mu;
+std::map<std::string, Entry> g_modules;   // key: device:arch:hash
+
+bool compile(const std::string& src, const std::string& arch, std::vector<char>& code, std::string* err) {
+    const char* hdrs[] = {wost_embedded_wost_h, wost_embedded_wost_device_h, wost_embedded_wost_walk_h};
+    const char* names[] = {"wost.h", "wost_device.h", "wost_walk.h"};
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "wost_walk_jit.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
+        *err = "hiprtcCreateProgram failed";
+        return false;
+    }
+    std::string arch_opt = "--offload-arch=" + arch;
+    const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt",
+                          "-ffp-contract=fast-honor-pragmas"};
+    hiprtcResult rc = hiprtcCompileProgram(prog, 5, opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n + 1, '\0');
+        if (n) hiprtcGetProgramLog(prog, &log[0]);
+        *err = std::string("hiprtc: ") + hiprtcGetErrorString(rc) + ": " + log.c_str();
+        hiprtcDestroyProgram(&prog);
+        return false;
+    }
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code.resize(n);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    return true;
+}
+
+}  // namespace
+
+std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors) {
+    const bool neu = mode == 2 || mode == 3 || mode == 5;
+    const bool src = mode == 1 || mode == 3 || mode == 4 || mode == 5;
+    const bool delta = mode == 4 || mode == 5;
+    const DField& fG = hdr.field[SLOT_G];
+    const DField& fF = hdr.field[SLOT_F];
+    const DField& fS = hdr.field[SLOT_SIGMA];
+    const DField& fA = hdr.field[SLOT_ALPHA];
+    std::ostringstream o;
+    o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
+      << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n";
+    o << "    __device__ __forceinline__ bool has_g() const { return " << (fG.present ? "true" : "false") << "; }\n";
+    o << "    __device__ __forceinline__ float g(float x, float y) const {\n"
+      << (fG.present ? value_body(fG, terms, factors) : "        return 0.0f;\n") << "    }\n";
+    o << "    __device__ __forceinline__ float f(float x, float y) const {\n"
+      << (fF.present ? value_body(fF, terms, factors) : "        return 0.0f;\n") << "    }\n";
+    o << "    __device__ __forceinline__ float sigma(float x, float y) const {\n"
+      << (fS.present ? value_body(fS, terms, factors) : "        return 0.0f;\n") << "    }\n";
+    o << "    __device__ __forceinline__ float alpha(float x, float y) const {\n"
+      << (fA.present ? value_body(fA, terms, factors) : "        return 1.0f;\n") << "    }\n";
+    o << "    __device__ __forceinline__ wost::Jet alpha_jet(float x, float y) const {\n"
+      << (fA.present ? jet_body(fA, terms, factors) : "        return wost::jet_const(1.0f);\n") << "    }\n";
+    o << "    __device__ __forceinline__ bool detached() const { return "
+      << ((fA.flags & WOST_FIELD_DETACHED) ? "true" : "false") << "; }\n";
+    o << "    __device__ __forceinline__ float sigma_bar() const { return " << lit(hdr.sigma_bar) << "; }\n";
+    o << "    __device__ __forceinline__ float sqrt_sigma_bar() const { return " << lit(hdr.sqrt_sigma_bar) << "; }\n";
+    o << "    __device__ __forceinline__ float inv_sigma_bar() const { return " << lit(hdr.inv_sigma_bar) << "; }\n";
+    o << "    __device__ __forceinline__ float inv_i0(float x) const {\n        const float ca[" << kChebA << "] = {";
+    for (int k = 0; k < kChebA; ++k) o << (k ? ", " : "") << lit(hdr.cheb_a[k]);
+    o << "};\n        const float cb[" << kChebB << "] = {";
+    for (int k = 0; k < kChebB; ++k) o << (k ? ", " : "") << lit(hdr.cheb_b[k]);
+    o << "};\n        return wost::inv_i0(ca, cb, x);\n    }\n};\n}  // namespace\n\n";
+    o << "extern \"C\" __global__ void __launch_bounds__(wost::kWalkBlock, 6)\n"
+      << "wost_walk_jit(const wost::WalkArgs A) {\n"
+      << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
+      << "    const GenFields fld;\n"
+      << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
+      << (delta ? "true" : "false") << ">(A, fld, smem);\n}\n";
+    return o.str();
+}
+
+bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        *err = "hipGetDeviceProperties failed";
+        return false;
+    }
+    std::string arch = prop.gcnArchName;
+    arch = arch.substr(0, arch.find(':'));
+    // the embedded headers are part of the key: a rebuilt library never reuses stale code
+    const uint64_t h = fnv1a(source + "|" + arch + "|" + wost_embedded_wost_h + wost_embedded_wost_device_h +
+                             wost_embedded_wost_walk_h);
+    char hex[32];
+    std::snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)h);
+    const std::string key = std::to_string(device) + ":" + arch + ":" + hex;
+
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_modules.find(key);
+    if (it != g_modules.end()) {
+        *fn = it->second.fn;
+        return true;
+    }
+    std::vector<char> code;
+    const std::string dir = cache_dir();
+    const std::string name = std::string("walk_") + arch + "_" + hex + ".hsaco";
+    if (dir.empty() || !read_file(dir + "/" + name, code)) {
+        if (!compile(source, arch, code, err)) return false;
+        write_file_atomic(dir, name, code);
+    }
+    Entry e;
+    if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess) {
+        *err = "hipModuleLoadData failed";
+        return false;
+    }
+    if (hipModuleGetFunction(&e.fn, e.mod, "wost_walk_jit") != hipSuccess) {
+        *err = "hipModuleGetFunction(wost_walk_jit) failed";
+        return false;
+    }
+    g_modules[key] = e;
+    *fn = e.fn;
+    return true;
+}
+
+}  // namespace wost

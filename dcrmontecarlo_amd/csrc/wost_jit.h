@@ -1,0 +1,29 @@
+// wost_jit.h -- field-specialised walk kernels compiled at run time (hiprtc).
+//
+// The precompiled walk kernel interprets each handle's coefficient fields
+// from a program buffer (a term/factor loop with a kind switch per factor).
+// For a given handle and kernel variant, libwost instead generates HIP source
+// in which the fields are straight-line calls to the same per-kind functions
+// (wost_device.h) with their parameters as literals, compiles it for the
+// device's gfx target with hiprtc, caches the code object (in memory and on
+// disk) and launches it with the same WalkArgs. Results are identical to the
+// interpreted kernel; the interpretation overhead disappears.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "wost_device.h"
+
+namespace wost {
+
+// HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
+// (wost_internal.h WalkMode) with the fields of `prog` compiled in.
+std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors);
+
+// Compiles (or fetches from the caches) the source for `device` and returns
+// the kernel. On failure returns false and a message in *err.
+bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err);
+
+}  // namespace wost

@@ -1,17 +1,9 @@
-// wost_kernels.hip -- gfx950 kernels of the Walk-on-Stars hot path.
+// wost_kernels.hip -- precompiled gfx950 kernels of the Walk-on-Stars hot path.
 //
-// wost_walk_kernel restates the per-walk loop of WostSolver_2D._solveUnified
-// (reference: solvers/WoStSolver.py:182-311) as one walk per lane:
-//  * persistent waves, each lane holding one walk's state in registers;
-//  * when walks finish, the wave re-fills those lanes by __ballot /
-//    __popcll rank from a chunk of walk ids it dequeued with one atomic
-//    (active-mask compaction, so short walks never idle a lane for long);
-//  * polyline vertices and the sampler's inverse-CDF table staged in LDS
-//    (wave-uniform segment loops read them as LDS broadcasts);
-//  * coefficient-field programs read through the constant address space
-//    with uniform indices (scalar loads);
-//  * Philox4x32-10 counters derived from (seed, walk id, step), no RNG state
-//    in memory.
+// wost_walk_kernel<NEU,SRC,DELTA>: the walk loop of wost_walk.h with the
+// coefficient fields interpreted from a program buffer read through the
+// constant address space with uniform indices (scalar loads). wost_jit.cpp
+// builds the same loop with the fields compiled in.
 // Per-walk results go to HBM; wost_block_reduce then sums them per block of
 // WOST_BLOCK_WALKS walks in a fixed order (deterministic, GPU-count
 // independent).
@@ -83,209 +75,51 @@ struct ProgView {
     }
 };
 
-constexpr size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
+// Fields read from the program buffer (the precompiled, interpreted path).
+struct InterpFields {
+    ProgView P;
+    DField fG, fF, fS, fA;
+    bool det;
+    float sb, sqsb, isb;
+    FloatsC ca, cb;
+    __device__ __forceinline__ explicit InterpFields(const char* prog) : P(prog) {
+        fG = P.field(SLOT_G);
+        fF = P.field(SLOT_F);
+        fS = P.field(SLOT_SIGMA);
+        fA = P.field(SLOT_ALPHA);
+        det = (fA.flags & WOST_FIELD_DETACHED) != 0;
+        sb = P.hdr->sigma_bar;
+        sqsb = P.hdr->sqrt_sigma_bar;
+        isb = P.hdr->inv_sigma_bar;
+        ca.p = (cptr<float>)P.hdr->cheb_a;
+        cb.p = (cptr<float>)P.hdr->cheb_b;
+    }
+    __device__ __forceinline__ bool has_g() const { return fG.present != 0; }
+    __device__ __forceinline__ float g(float x, float y) const { return P.value(fG, x, y); }
+    __device__ __forceinline__ float f(float x, float y) const { return P.value(fF, x, y); }
+    __device__ __forceinline__ float sigma(float x, float y) const { return fS.present ? P.value(fS, x, y) : 0.0f; }
+    __device__ __forceinline__ float alpha(float x, float y) const { return P.value(fA, x, y); }
+    __device__ __forceinline__ Jet alpha_jet(float x, float y) const { return P.jet(fA, x, y); }
+    __device__ __forceinline__ bool detached() const { return det; }
+    __device__ __forceinline__ float sigma_bar() const { return sb; }
+    __device__ __forceinline__ float sqrt_sigma_bar() const { return sqsb; }
+    __device__ __forceinline__ float inv_sigma_bar() const { return isb; }
+    __device__ __forceinline__ float inv_i0(float x) const { return wost::inv_i0(ca, cb, x); }
+};
 
-size_t walk_lds_bytes(int mode, int nd, int nn, int n_points) {
-    bool neu = mode == MODE_MIXED || mode == MODE_MIXED_POISSON || mode == MODE_MIXED_DELTA;
-    bool src = mode == MODE_POISSON || mode == MODE_MIXED_POISSON || mode == MODE_DELTA ||
-               mode == MODE_MIXED_DELTA;
-    size_t b = align16(sizeof(float2) * (size_t)nd);
-    if (neu) b += align16(sizeof(float2) * (size_t)nn);
-    if (src) b += align16(sizeof(float) * WOST_SAMPLER_TABLE_N);
-    if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
-    return b;
-}
-
-// One walk-step of _solveUnified (solvers/WoStSolver.py:206-291) for every
-// active lane, with the finish/refill logic of loops 1-2 (:182-188, :294-311)
-// around it.
 #ifndef WOST_WALK_MIN_WAVES
 #define WOST_WALK_MIN_WAVES 6   // 6 waves/SIMD: measured best (tools/ab_bench.sh)
 #endif
+
+// One walk-step of _solveUnified (solvers/WoStSolver.py:206-291) for every
+// active lane, with the finish/refill logic of loops 1-2 (:182-188, :294-311)
+// around it: see wost_walk.h.
 template <bool NEU, bool SRC, bool DELTA>
 __global__ void __launch_bounds__(kWalkBlock, WOST_WALK_MIN_WAVES)
 wost_walk_kernel(const WalkArgs A) {
-    // the walk's position updates round op by op like the reference (torch CPU
-    // has no FMA contraction); the field math it calls keeps FMAs
-#pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2* sD = reinterpret_cast<float2*>(smem);
-    float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
-    float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
-                                         (NEU ? align16(sizeof(float2) * (size_t)A.nn) : 0));
-    float2* sP = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(sT) +
-                                           (SRC ? align16(sizeof(float) * WOST_SAMPLER_TABLE_N) : 0));
-    const bool points_in_lds = A.n_points <= kLdsPointsMax;
-
-    for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
-    if (NEU)
-        for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
-    if (SRC)
-        for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
-    if (points_in_lds)
-        for (int i = threadIdx.x; i < A.n_points; i += blockDim.x) sP[i] = A.points[i];
-    __syncthreads();
-
-    const ProgView P(A.prog);
-    const DField fG = P.field(SLOT_G);
-    const DField fF = P.field(SLOT_F);
-    const DField fS = P.field(SLOT_SIGMA);
-    const DField fA = P.field(SLOT_ALPHA);
-    const bool detached = (fA.flags & WOST_FIELD_DETACHED) != 0;
-    const float sigma_bar = P.hdr->sigma_bar;
-    const float sqrt_sb = P.hdr->sqrt_sigma_bar;
-    const float inv_sb = P.hdr->inv_sigma_bar;
-    const FloatsC cheb_a{(cptr<float>)P.hdr->cheb_a};
-    const FloatsC cheb_b{(cptr<float>)P.hdr->cheb_b};
-
-    const int lane = threadIdx.x & 63;
-    const uint64_t lanebit = 1ull << lane;
-    const uint64_t lanes_below = lanebit - 1ull;
-
-    // wave-uniform work-queue state
-    uint64_t c_next = 0, c_end = 0;
-    bool exhausted = false;
-
-    // per-lane walk state (solvers/WoStSolver.py:188-195)
-    bool active = false;
-    uint64_t wid = 0;
-    float px = 0.f, py = 0.f;
-    float dD = 1.0f;            // dDirichlet seeded with 1.0 (:190, quirk Q12)
-    int k = 0;                  // step_count
-    bool onB = false;           // onBoundary
-    float nx = 0.f, ny = 1.f;   // normal
-    float w = 1.f;              // attenuation_coef
-    float ax = 1.f;             // alpha(current_point), cached
-    float total = 0.f;          // this walk's contributions
-
-    for (;;) {
-        // --- walk termination: while-condition of :206, boundary term :295-298
-        if (active && !((k < A.max_steps) && (dD > A.eps))) {
-            float g = fG.present ? P.value(fG, px, py) : 0.0f;
-            if (DELTA) g = g * w;
-            total = total + g;
-            const int64_t li = (int64_t)(wid - (uint64_t)A.wid_begin);
-            A.out_val[li] = total;
-            A.out_steps[li] = (uint32_t)k;
-            active = false;
-        }
-
-        // --- refill idle lanes from the wave's chunk (active-mask compaction)
-        uint64_t need = __ballot(!active);
-        while (need != 0ull && !exhausted) {
-            if (c_next >= c_end) {
-                unsigned long long c = 0;
-                if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)A.chunk);
-                c = __shfl(c, 0);
-                if (c >= (unsigned long long)A.count) {
-                    exhausted = true;
-                    break;
-                }
-                c_next = c;
-                c_end = c + (uint64_t)A.chunk;
-                if (c_end > (uint64_t)A.count) c_end = (uint64_t)A.count;
-            }
-            const uint64_t avail = c_end - c_next;
-            const uint32_t n = (uint32_t)__popcll(need);
-            const uint32_t take = avail < (uint64_t)n ? (uint32_t)avail : n;
-            const uint32_t rank = (uint32_t)__popcll(need & lanes_below);
-            if ((need & lanebit) && rank < take) {
-                wid = (uint64_t)A.wid_begin + c_next + rank;
-                // pid = wid / W without a 64-bit integer division: a double
-                // estimate (exact operands below 2^53) and one correction
-                uint64_t pid = (uint64_t)((double)wid * A.inv_walks_per_point);
-                const int64_t rem = (int64_t)(wid - pid * (uint64_t)A.walks_per_point);
-                if (rem < 0) --pid;
-                else if (rem >= A.walks_per_point) ++pid;
-                float2 q;
-                if (points_in_lds) q = sP[pid];
-                else q = A.points[pid];
-                px = q.x; py = q.y;
-                k = 0; dD = 1.0f; onB = false; nx = 0.f; ny = 1.f; w = 1.f; total = 0.f;
-                if (DELTA) ax = P.value(fA, px, py);
-                active = true;
-            }
-            c_next += take;
-            need = __ballot(!active);
-        }
-        if (!__any(active)) break;
-        // a freshly refilled walk may already fail the while-condition (eps >= 1,
-        // maxSteps == 0): it takes no step and is finished at the next iteration
-        if (!(active && (k < A.max_steps) && (dD > A.eps))) continue;
-
-        // --- one walk-step (:206-291)
-        const float dd = poly_distance(sD, A.nd, px, py);           // :208
-        float r;
-        if (NEU) {
-            const float dn = silhouette_distance(sN, A.nn, px, py);  // :211
-            const float m = dn < dd ? dn : dd;                       // Python min()
-            r = m > A.rmin ? m : A.rmin;                             // Python max() (:212)
-        } else {
-            r = dd > A.rmin ? dd : A.rmin;                           // :215
-        }
-
-        const U4 rn = philox4x32_10(U4{(uint32_t)k, 0u, (uint32_t)wid, (uint32_t)(wid >> 32)},
-                                    A.key0, A.key1);
-        float theta = (u01(rn.x) * 2.0f) * kPiF;                     // :226
-        if (NEU && onB) theta = theta / 2.0f + atan2f(ny, nx);       // :227-228 (quirk Q2)
-        const float cs = f_cos(theta), sn = f_sin(theta);            // :230-232
-
-        float xnx, xny;
-        if (NEU) {                                                   // :235-236
-            const Hit h = intersect_polylines(sN, A.nn, px, py, cs, sn, r);
-            xnx = h.x; xny = h.y; nx = h.nx; ny = h.ny; onB = h.hit;
-        } else {                                                     // :238-239
-            xnx = px + r * cs;
-            xny = py + r * sn;
-        }
-
-        float yx = xnx, yy = xny;
-        bool clipped = false;
-        float gnorm = 0.f;
-        Jet aj{0.f, 0.f, 0.f, 0.f};
-        if (SRC) {                                                   // :242-258
-            const float rs = sample_rho(sT, u01(rn.y)) * r;          // :244 (sampler, quirks Q3-Q5)
-            yx = px + rs * cs;                                       // :245 (quirk Q13)
-            yy = py + rs * sn;
-            const float e1x = yx - px, e1y = yy - py;
-            const float e2x = xnx - px, e2y = xny - py;
-            clipped = sqrtf(e1x * e1x + e1y * e1y) > sqrtf(e2x * e2x + e2y * e2y);  // :248
-            if (clipped) { yx = xnx; yy = xny; }
-            if (DELTA) {
-                gnorm = inv_sb * (1.0f - inv_i0(cheb_a, cheb_b, r * sqrt_sb));  // solvers/utils.py:43-44
-                aj = P.jet(fA, yx, yy);
-            }
-            float c = 0.0f;
-            if (!clipped) {
-                const float f = P.value(fF, yx, yy);
-                if (DELTA)
-                    c = (f * gnorm) * f_rcp(f_sqrt(aj.v * ax)) * w;  // :253-254
-                else
-                    c = f * ((r * r) / 4.0f);                        // :256, utils.py:61
-            }
-            total = total + c;                                       // :258
-        }
-
-        if (DELTA) {                                                 // :271-284
-            const float mu = u01(rn.z);
-            if (mu > sigma_bar * gnorm) {
-                const float an = clipped ? aj.v : P.value(fA, xnx, xny);
-                w = w * f_sqrt(f_div(an, ax));                       // :277
-                px = xnx; py = xny; ax = an;
-            } else {
-                const float sg = fS.present ? P.value(fS, yx, yy) : 0.0f;
-                const float spv = sigma_prime_from(aj, sg, detached);    // :281
-                float sc = 1.0f - spv * inv_sb;
-                sc = (0.0f > sc) ? 0.0f : sc;                        // Python max(., 0.0) (:282)
-                w = (w * f_sqrt(f_div(aj.v, ax))) * sc;              // :283
-                px = yx; py = yy; ax = aj.v;
-            }
-        } else {
-            px = xnx; py = xny;                                      // :287
-        }
-        k += 1;                                                      // :291
-        dD = dd;   // the loop tests the distance of the pre-step point (quirk Q7)
-    }
+    const InterpFields fld(A.prog);
+    walk_body<NEU, SRC, DELTA>(A, fld, smem);
 }
 
 hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu) {

@@ -1,0 +1,236 @@
+// wost_walk.h -- the walk loop of WostSolver_2D._solveUnified
+// (reference: solvers/WoStSolver.py:182-311) as a device function template,
+// instantiated by the precompiled kernels (wost_kernels.hip, fields read from
+// a program buffer) and by the hiprtc-specialised kernels (wost_jit.cpp,
+// fields compiled in). Compiled by hipcc and by hiprtc: no system headers.
+//
+// One walk per lane:
+//  * persistent waves; each lane holds one walk's state in registers;
+//  * when walks finish, the wave re-fills those lanes by __ballot / __popcll
+//    rank from a chunk of walk ids it dequeued with one atomic (active-mask
+//    compaction, so short walks never idle a lane for long);
+//  * polyline vertices, the sampler's inverse-CDF table and (up to 1024) query
+//    points staged in LDS; the segment loops are wave-uniform (LDS broadcasts);
+//  * Philox4x32-10 counters derived from (seed, walk id, step): no RNG state.
+#pragma once
+
+#include "wost_device.h"
+
+namespace wost {
+
+// Arguments of the walk kernel, passed by value in the kernarg segment.
+struct WalkArgs {
+    const float2* points;        // [n_points] query points
+    const float2* dverts;        // Dirichlet polyline vertices
+    const float2* nverts;        // Neumann polyline vertices (may be null)
+    const float* table;          // sampler inverse-CDF nodes (may be null)
+    const char* prog;            // DProgram + terms + factors (interpreted fields)
+    float* out_val;              // [count] per-walk estimate
+    uint32_t* out_steps;         // [count] per-walk step count
+    unsigned long long* counter; // work-queue head (zeroed before launch)
+    int64_t wid_begin;           // global id of local walk 0
+    int64_t count;               // walks in this launch
+    int64_t walks_per_point;     // W: point of global walk g is g / W
+    int32_t nd, nn;              // vertex counts
+    int32_t max_steps;
+    float eps;
+    float rmin;                  // eps / 2 (solvers/WoStSolver.py:167)
+    uint32_t key0, key1;         // Philox key = seed
+    int32_t chunk;               // walks claimed per work-queue dequeue
+    int32_t n_points;            // query points (staged in LDS when <= kLdsPointsMax)
+    double inv_walks_per_point;  // 1/W for the point index of a walk id
+};
+
+constexpr int kWalkBlock = 256;
+constexpr int kLdsPointsMax = 1024;
+
+WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
+
+// Bytes of dynamic LDS a walk-kernel workgroup needs.
+WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points) {
+    size_t b = align16(sizeof(float2) * (size_t)nd);
+    if (neu) b += align16(sizeof(float2) * (size_t)nn);
+    if (src) b += align16(sizeof(float) * WOST_SAMPLER_TABLE_N);
+    if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
+    return b;
+}
+
+// The Fields policy F provides: has_g(), g(x,y), f(x,y), sigma(x,y),
+// alpha(x,y), alpha_jet(x,y), detached(), sigma_bar(), sqrt_sigma_bar(),
+// inv_sigma_bar(), inv_i0(x).
+template <bool NEU, bool SRC, bool DELTA, class F>
+__device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
+    // the walk's position updates round op by op like the reference (torch CPU
+    // has no FMA contraction); the field math it calls keeps its own setting
+#pragma clang fp contract(off)
+    float2* sD = reinterpret_cast<float2*>(smem);
+    float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
+    float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
+                                         (NEU ? align16(sizeof(float2) * (size_t)A.nn) : 0));
+    float2* sP = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(sT) +
+                                           (SRC ? align16(sizeof(float) * WOST_SAMPLER_TABLE_N) : 0));
+    const bool points_in_lds = A.n_points <= kLdsPointsMax;
+
+    for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
+    if (NEU)
+        for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
+    if (SRC)
+        for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
+    if (points_in_lds)
+        for (int i = threadIdx.x; i < A.n_points; i += blockDim.x) sP[i] = A.points[i];
+    __syncthreads();
+
+    const float sigma_bar = fld.sigma_bar();
+    const float inv_sb = fld.inv_sigma_bar();
+    const float sqrt_sb = fld.sqrt_sigma_bar();
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t lanebit = 1ull << lane;
+    const uint64_t lanes_below = lanebit - 1ull;
+
+    // wave-uniform work-queue state
+    uint64_t c_next = 0, c_end = 0;
+    bool exhausted = false;
+
+    // per-lane walk state (solvers/WoStSolver.py:188-195)
+    bool active = false;
+    uint64_t wid = 0;
+    float px = 0.f, py = 0.f;
+    float dD = 1.0f;            // dDirichlet seeded with 1.0 (:190, quirk Q12)
+    int k = 0;                  // step_count
+    bool onB = false;           // onBoundary
+    float nx = 0.f, ny = 1.f;   // normal
+    float w = 1.f;              // attenuation_coef
+    float ax = 1.f;             // alpha(current_point), cached
+    float total = 0.f;          // this walk's contributions
+
+    for (;;) {
+        // --- walk termination: while-condition of :206, boundary term :295-298
+        if (active && !((k < A.max_steps) && (dD > A.eps))) {
+            float g = fld.has_g() ? fld.g(px, py) : 0.0f;
+            if (DELTA) g = g * w;
+            total = total + g;
+            const int64_t li = (int64_t)(wid - (uint64_t)A.wid_begin);
+            A.out_val[li] = total;
+            A.out_steps[li] = (uint32_t)k;
+            active = false;
+        }
+
+        // --- refill idle lanes from the wave's chunk (active-mask compaction)
+        uint64_t need = __ballot(!active);
+        while (need != 0ull && !exhausted) {
+            if (c_next >= c_end) {
+                unsigned long long c = 0;
+                if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)A.chunk);
+                c = __shfl(c, 0);
+                if (c >= (unsigned long long)A.count) {
+                    exhausted = true;
+                    break;
+                }
+                c_next = c;
+                c_end = c + (uint64_t)A.chunk;
+                if (c_end > (uint64_t)A.count) c_end = (uint64_t)A.count;
+            }
+            const uint64_t avail = c_end - c_next;
+            const uint32_t n = (uint32_t)__popcll(need);
+            const uint32_t take = avail < (uint64_t)n ? (uint32_t)avail : n;
+            const uint32_t rank = (uint32_t)__popcll(need & lanes_below);
+            if ((need & lanebit) && rank < take) {
+                wid = (uint64_t)A.wid_begin + c_next + rank;
+                // pid = wid / W without a 64-bit integer division: a double
+                // estimate (exact operands below 2^53) and one correction
+                uint64_t pid = (uint64_t)((double)wid * A.inv_walks_per_point);
+                const int64_t rem = (int64_t)(wid - pid * (uint64_t)A.walks_per_point);
+                if (rem < 0) --pid;
+                else if (rem >= A.walks_per_point) ++pid;
+                float2 q;
+                if (points_in_lds) q = sP[pid];
+                else q = A.points[pid];
+                px = q.x; py = q.y;
+                k = 0; dD = 1.0f; onB = false; nx = 0.f; ny = 1.f; w = 1.f; total = 0.f;
+                if (DELTA) ax = fld.alpha(px, py);
+                active = true;
+            }
+            c_next += take;
+            need = __ballot(!active);
+        }
+        if (!__any(active)) break;
+        // a freshly refilled walk may already fail the while-condition (eps >= 1,
+        // maxSteps == 0): it takes no step and is finished at the next iteration
+        if (!(active && (k < A.max_steps) && (dD > A.eps))) continue;
+
+        // --- one walk-step (:206-291)
+        const float dd = poly_distance(sD, A.nd, px, py);           // :208
+        float r;
+        if (NEU) {
+            const float dn = silhouette_distance(sN, A.nn, px, py);  // :211
+            const float m = dn < dd ? dn : dd;                       // Python min()
+            r = m > A.rmin ? m : A.rmin;                             // Python max() (:212)
+        } else {
+            r = dd > A.rmin ? dd : A.rmin;                           // :215
+        }
+
+        const U4 rn = philox4x32_10(U4{(uint32_t)k, 0u, (uint32_t)wid, (uint32_t)(wid >> 32)},
+                                    A.key0, A.key1);
+        float theta = (u01(rn.x) * 2.0f) * kPiF;                     // :226
+        if (NEU && onB) theta = theta / 2.0f + atan2f(ny, nx);       // :227-228 (quirk Q2)
+        const float cs = f_cos(theta), sn = f_sin(theta);            // :230-232
+
+        float xnx, xny;
+        if (NEU) {                                                   // :235-236
+            const Hit h = intersect_polylines(sN, A.nn, px, py, cs, sn, r);
+            xnx = h.x; xny = h.y; nx = h.nx; ny = h.ny; onB = h.hit;
+        } else {                                                     // :238-239
+            xnx = px + r * cs;
+            xny = py + r * sn;
+        }
+
+        float yx = xnx, yy = xny;
+        bool clipped = false;
+        float gnorm = 0.f;
+        Jet aj{0.f, 0.f, 0.f, 0.f};
+        if (SRC) {                                                   // :242-258
+            const float rs = sample_rho(sT, u01(rn.y)) * r;          // :244 (sampler, quirks Q3-Q5)
+            yx = px + rs * cs;                                       // :245 (quirk Q13)
+            yy = py + rs * sn;
+            const float e1x = yx - px, e1y = yy - py;
+            const float e2x = xnx - px, e2y = xny - py;
+            clipped = sqrtf(e1x * e1x + e1y * e1y) > sqrtf(e2x * e2x + e2y * e2y);  // :248
+            if (clipped) { yx = xnx; yy = xny; }
+            if (DELTA) {
+                gnorm = inv_sb * (1.0f - fld.inv_i0(r * sqrt_sb));   // solvers/utils.py:43-44
+                aj = fld.alpha_jet(yx, yy);
+            }
+            float c = 0.0f;
+            if (!clipped) {
+                const float f = fld.f(yx, yy);
+                if (DELTA)
+                    c = (f * gnorm) * f_rcp(f_sqrt(aj.v * ax)) * w;  // :253-254
+                else
+                    c = f * ((r * r) / 4.0f);                        // :256, utils.py:61
+            }
+            total = total + c;                                       // :258
+        }
+
+        if (DELTA) {                                                 // :271-284
+            const float mu = u01(rn.z);
+            if (mu > sigma_bar * gnorm) {
+                const float an = clipped ? aj.v : fld.alpha(xnx, xny);
+                w = w * f_sqrt(f_div(an, ax));                       // :277
+                px = xnx; py = xny; ax = an;
+            } else {
+                const float spv = sigma_prime_from(aj, fld.sigma(yx, yy), fld.detached());  // :281
+                float sc = 1.0f - spv * inv_sb;
+                sc = (0.0f > sc) ? 0.0f : sc;                        // Python max(., 0.0) (:282)
+                w = (w * f_sqrt(f_div(aj.v, ax))) * sc;              // :283
+                px = yx; py = yy; ax = aj.v;
+            }
+        } else {
+            px = xnx; py = xny;                                      // :287
+        }
+        k += 1;                                                      // :291
+        dD = dd;   // the loop tests the distance of the pre-step point (quirk Q7)
+    }
+}
+
+}  // namespace wost

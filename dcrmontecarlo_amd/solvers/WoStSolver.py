@@ -189,6 +189,11 @@ class WostSolver_2D:
         self.last_timing = self.timing()
         return bs
 
+    def set_jit(self, enable: bool):
+        """Use the field-specialised (hiprtc) walk kernel (default) or the precompiled
+        kernel that interprets the fields. Both give identical results."""
+        _lib.check(_lib.lib.wost_set_jit(self._h, 1 if enable else 0), "wost_set_jit")
+
     def num_blocks(self, n_points: int, nWalks: int) -> int:
         return int(_lib.lib.wost_num_blocks(int(n_points), int(nWalks)))
 

@@ -15,7 +15,16 @@
 #ifndef WOST_H
 #define WOST_H
 
+#if defined(__HIPCC_RTC__)
+/* compiled by hiprtc as part of a JIT-specialised walk kernel: no system headers */
+typedef unsigned char uint8_t;
+typedef int int32_t;
+typedef unsigned int uint32_t;
+typedef long long int64_t;
+typedef unsigned long long uint64_t;
+#else
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -132,6 +141,9 @@ typedef struct {
     int32_t grid_blocks;        /* workgroups per walk-kernel launch            */
     uint64_t total_steps;       /* walk-steps executed in the last solve         */
     uint64_t total_walks;
+    int32_t jit;                /* 1: field-specialised (hiprtc) walk kernel,
+                                   0: precompiled kernel interpreting the fields */
+    int32_t reserved;
 } wost_timing;
 
 int wost_version(void);
@@ -174,6 +186,13 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points,
                float* walk_values, uint32_t* walk_steps);
 
 int wost_last_timing(const wost_handle* h, wost_timing* out);
+
+/* Walk kernels: by default libwost compiles a field-specialised walk kernel per
+ * handle and kernel variant with hiprtc (cached in memory and in
+ * $WOST_JIT_CACHE, default ~/.cache/wost) and falls back to the precompiled
+ * interpreting kernel if that fails. enable = 0 forces the precompiled kernel
+ * (also: environment WOST_JIT=0). Both give identical results. */
+int wost_set_jit(wost_handle* h, int32_t enable);
 
 /* Device evaluation of the handle's fields at points (for tests and for the
  * host API): which = 0 g, 1 f, 2 sigma, 3 alpha (value, d/dx, d/dy, Laplacian

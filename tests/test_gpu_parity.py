@@ -235,6 +235,26 @@ def test_laplace_converges_to_exact(gpu_available):
     assert np.sqrt(np.mean(z ** 2)) < 3.0
 
 
+@pytest.mark.parametrize("name", SCEN)
+def test_jit_kernel_matches_interpreted_kernel(gpu_available, name):
+    """The hiprtc field-specialised walk kernel and the precompiled kernel that
+    interprets the field program give bit-identical per-walk results."""
+    sc, s = _solver_for(name)
+    pts = sc.points[:8]
+    W = 2048
+    u1, h1 = s.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=3, return_history=True)
+    assert s.last_timing["jit"] == 1, "the field-specialised kernel did not build"
+    s.set_jit(False)
+    u0, h0 = s.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=3, return_history=True)
+    assert s.last_timing["jit"] == 0
+    v1 = np.array([w["value"] for i in range(len(pts)) for w in h1[i]], np.float32)
+    v0 = np.array([w["value"] for i in range(len(pts)) for w in h0[i]], np.float32)
+    s1 = np.array([w["steps"] for i in range(len(pts)) for w in h1[i]])
+    s0 = np.array([w["steps"] for i in range(len(pts)) for w in h0[i]])
+    assert np.array_equal(s1, s0)
+    assert np.array_equal(v1.view(np.uint32), v0.view(np.uint32)) or np.array_equal(v1, v0)
+
+
 # ---------------------------------------------------------------- full-size properties
 def test_dcr_full_size_linearity(gpu_available):
     """C4 at its full size (48 electrodes x 1M walks): the walk does not depend on the

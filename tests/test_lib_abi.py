@@ -30,7 +30,7 @@ def test_struct_layouts():
     assert ctypes.sizeof(_lib.WostTerm) == 12
     assert ctypes.sizeof(_lib.WostPolyline) == 16
     assert ctypes.sizeof(_lib.WostProblem) == 80
-    assert ctypes.sizeof(_lib.WostTiming) == 48
+    assert ctypes.sizeof(_lib.WostTiming) == 56
 
 
 def test_fails_loudly_without_a_device():
