@@ -32,8 +32,8 @@ sys.path.insert(0, REPO)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--walks", type=int, default=1_000_000, help="walks per electrode")
     ap.add_argument("--electrodes", type=int, default=48)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
@@ -60,6 +60,17 @@ def cpu_baseline(sc, budget_s: float):
     return {"value": float(s.sum()) / dt, "unit": "walk-steps/sec", "cores": threads, "kind": "port",
             "sample": f"dcr_dipole {len(pts)} electrodes x {w} walks ({int(s.sum())} walk-steps, {dt:.1f} s), "
                       f"oracle/wost_oracle.c with {threads} OpenMP threads"}
+
+
+def measured_traffic():
+    """HBM bytes per walk-kernel launch from the committed rocprofv3 PMC passes of this
+    workload (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE), if present."""
+    path = os.path.join(REPO, "profiles", "traffic_dcr_dipole.json")
+    try:
+        with open(path) as f:
+            return json.load(f)["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def main():
@@ -106,12 +117,14 @@ def main():
     steps_local = 0
     kernel_ms = 0.0
     launches = 0
+    jit = 0
     sums = None
     for k in range(args.steps):
         sums, t = one_step(k)
         steps_local += int(t["total_steps"])
         kernel_ms += float(t["walk_kernel_ms"])
         launches += int(t["n_launches"])
+        jit = int(t["jit"])
     barrier_sync()
     elapsed = time.perf_counter() - t0
 
@@ -155,10 +168,13 @@ def main():
                        "parallelism": f"walk-block shards x{world}, RCCL all_gather of block sums"},
             "roofline": {"bound": "valu", "achieved": ach_tflops, "peak": perfmodel.FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": ach_tflops / perfmodel.FP32_PEAK_TFLOPS, "traffic": None,
-                         "model_flops_per_step": fps, "kernel": "wost_walk_kernel<true,true,true>",
+                         "model_flops_per_step": fps,
+                         "kernel": "wost_walk_jit (hiprtc field-specialised, mixed+delta)" if jit
+                         else "wost_walk_kernel<true,true,true> (precompiled)",
                          "kernel_ms_per_launch": kernel_ms / max(launches, 1)},
             "roofline_hbm": {"bound": "hbm", "achieved": ach_gbs, "peak": perfmodel.HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": ach_gbs / perfmodel.HBM_PEAK_GBS, "traffic": None},
+                             "frac": ach_gbs / perfmodel.HBM_PEAK_GBS, "traffic": measured_traffic(),
+                             "algorithmic_bytes_per_launch": bytes_per_launch},
             "u_checksum": float(np.sum(mean)),
         }
         if not args.no_cpu and world == 1:

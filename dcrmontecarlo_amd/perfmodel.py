@@ -68,6 +68,9 @@ def flops_per_step(scenario) -> float:
 
 
 def hbm_bytes_per_walk() -> float:
-    """Algorithmic HBM traffic per walk: the point read (8 B) and the per-walk result
-    (value + step count, 8 B) written by the walk kernel and re-read by the block reduction."""
-    return 8.0 + 8.0 + 8.0
+    """Algorithmic HBM traffic of the walk kernel per walk: the per-walk result
+    (float value + uint32 step count) it writes. Geometry, sampler table, field
+    program and query points are read once per workgroup into LDS / the scalar
+    cache. (rocprofv3 on C4: WRITE_SIZE 413 MB per 48M-walk launch, FETCH_SIZE
+    0.4 MB after the gfx950 x2 correction -- profiles/r01_jit/.)"""
+    return 8.0

@@ -1,21 +1,32 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSVs per walk-kernel dispatch: instruction mix per
-wave-step and issue utilisation. Usage: tools/pmc_summary.py dir1 [dir2 ...]
-(walk-steps per dispatch are taken from the matching scenario_bench log if given
-with --steps-json)."""
+"""Per walk-kernel dispatch summary of rocprofv3 --pmc CSVs (one or more passes).
+Usage: tools/pmc_summary.py [--steps N] dir1 [dir2 ...]
+With --steps (walk-steps of one dispatch) also prints instructions per wave-step."""
+import argparse
 import collections
 import csv
-import sys
 
+ap = argparse.ArgumentParser()
+ap.add_argument("dirs", nargs="+")
+ap.add_argument("--steps", type=float, default=0.0)
+a = ap.parse_args()
 rows = collections.defaultdict(dict)
-for d in sys.argv[1:]:
+for d in a.dirs:
     for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        if "walk_kernel" not in r["Kernel_Name"]:
+        if "wost_walk" not in r["Kernel_Name"]:
             continue
-        key = (r["Dispatch_Id"] if False else None, r["Kernel_Name"].split("<")[1].split(">")[0], r["Grid_Size"])
-        rows[(d, r["Dispatch_Id"])]["kernel"] = r["Kernel_Name"].split("<")[1].split(">")[0]
-        rows[(d, r["Dispatch_Id"])]["vgpr"] = r["VGPR_Count"]
-        rows[(d, r["Dispatch_Id"])]["sgpr"] = r["SGPR_Count"]
-        rows[(d, r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
-for k, v in sorted(rows.items()):
-    print(k, {kk: (f"{vv:.4g}" if isinstance(vv, float) else vv) for kk, vv in v.items()})
+        k = r["Dispatch_Id"]
+        rows[k]["kernel"] = r["Kernel_Name"][:60]
+        rows[k]["grid"] = r["Grid_Size"]
+        rows[k][r["Counter_Name"]] = float(r["Counter_Value"])
+for k, v in sorted(rows.items(), key=lambda kv: int(kv[0])):
+    out = {kk: (f"{vv:.4g}" if isinstance(vv, float) else vv) for kk, vv in v.items()}
+    if a.steps and "SQ_INSTS_VALU" in v:
+        ws = a.steps / 64.0
+        out["VALU/wave-step"] = f"{v['SQ_INSTS_VALU'] / ws:.0f}"
+        out["SALU/wave-step"] = f"{v.get('SQ_INSTS_SALU', 0) / ws:.0f}"
+    if "FETCH_SIZE" in v:
+        out["fetch_bytes(x2 gfx950 wide-read correction)"] = f"{v['FETCH_SIZE'] * 1024 * 2:.4g}"
+    if "WRITE_SIZE" in v:
+        out["write_bytes"] = f"{v['WRITE_SIZE'] * 1024:.4g}"
+    print(k, out)
