@@ -41,25 +41,68 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(sc, budget_s: float):
-    """The CPU oracle (C, OpenMP over walks) on a bounded sample of the same survey."""
+CPU_SEED = 321
+ALPHA_BG = 1e2   # background conductivity of testGeophysicalScenario.py:39 (rho_bg = 0.01)
+
+
+def _point_stats(v, W):
+    v = v.astype(np.float64).reshape(-1, W)
+    return v.mean(axis=1), v.std(axis=1, ddof=1) / np.sqrt(W)
+
+
+def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
+    """The CPU oracle (C, OpenMP over walks) on a bounded sample of the same survey:
+    timed on the model solve (the cpu_baseline), then also run on the homogeneous
+    background so the sample yields the survey's apparent resistivities."""
     from oracle import oracle as O
 
     threads = min(16, len(os.sched_getaffinity(0)))
-    pb = O.Problem.from_scenario(sc, sigma_bar=10.0)
+    pb = O.Problem.from_scenario(sc, sigma_bar=sigma_bar)
     pts = sc.points
-    pb.solve_walks(pts, 1, sc.max_steps, sc.eps, 1, threads=threads)       # builds the sampler table
+    pb.solve_walks(pts, 2, sc.max_steps, sc.eps, 1, threads=threads)       # builds the sampler table
     w = 64
     while True:                                                             # grow the sample to the budget
         t0 = time.perf_counter()
-        _, s = pb.solve_walks(pts, w, sc.max_steps, sc.eps, 321, threads=threads)
+        v, s = pb.solve_walks(pts, w, sc.max_steps, sc.eps, CPU_SEED, threads=threads)
         dt = time.perf_counter() - t0
         if dt >= 0.5 * budget_s or w >= 1_000_000:
             break
         w = int(min(1_000_000, w * max(2.0, 0.8 * budget_s / max(dt, 1e-3))))
-    return {"value": float(s.sum()) / dt, "unit": "walk-steps/sec", "cores": threads, "kind": "port",
+    base = {"value": float(s.sum()) / dt, "unit": "walk-steps/s", "cores": threads, "kind": "port",
             "sample": f"dcr_dipole {len(pts)} electrodes x {w} walks ({int(s.sum())} walk-steps, {dt:.1f} s), "
                       f"oracle/wost_oracle.c with {threads} OpenMP threads"}
+    vh, _ = O.Problem.from_scenario(sc_h, sigma_bar=sigma_bar_h).solve_walks(pts, w, sc.max_steps, sc.eps, CPU_SEED,
+                                                                             threads=threads)
+    return base, w, _point_stats(v, w), _point_stats(vh, w)
+
+
+def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu):
+    """Apparent resistivity of the dipole-dipole line: the full GPU run's precision, and
+    the GPU vs the CPU reference on the same walks (same seeds) of the CPU sample."""
+    pairs = survey.dipole_dipole_pairs(len(gpu_full[0][0]))
+
+    def rho(model, bg):
+        dm = survey.potential_differences(model[0], model[1], pairs)
+        dh = survey.potential_differences(bg[0], bg[1], pairs)
+        return survey.apparent_resistivity(dm, dh, 1.0 / alpha_bg)
+
+    full = rho(gpu_full[0], gpu_full[1])
+    ok = full.resolved & np.isfinite(full.rho_a)
+    out = {"array": f"dipole-dipole, {len(pairs)} adjacent-electrode dipoles",
+           "rho_bg": 1.0 / alpha_bg,
+           "gpu_full": {"walks_per_electrode": int(gpu_full[2]), "resolved": int(ok.sum()),
+                        "mc_1sigma_rms": float(np.sqrt(np.mean(full.se[ok] ** 2))) if ok.any() else None,
+                        "rho_a_checksum": float(np.sum(full.rho_a[ok]))}}
+    if cpu_same is not None:
+        g, c = rho(*gpu_same), rho(*cpu_same)
+        cmp = survey.compare(g, c)
+        cmp_full = survey.compare(full, c)
+        out["vs_cpu_reference"] = {
+            "walks_per_electrode": int(w_cpu), "seed": CPU_SEED, "resolved": cmp["resolved"],
+            "rmse": cmp["rmse"], "cpu_mc_1sigma_rms": cmp["mc_1sigma"],
+            "rmse_over_1sigma": (cmp["rmse"] / cmp["mc_1sigma"]) if cmp["rmse"] is not None and cmp["mc_1sigma"] else None,
+            "gpu_full_rmse": cmp_full["rmse"]}
+    return out
 
 
 def measured_traffic():
@@ -89,6 +132,8 @@ def main():
     from dcrmontecarlo_amd import distributed as D
     from dcrmontecarlo_amd import perfmodel
     from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd import survey
+    from dcrmontecarlo_amd.solvers.WoStSolver import stats_from_sums
 
     sc = S.dcr_dipole(n_electrodes=args.electrodes, n_walks=args.walks)
     solver = sc.solver(device=local)
@@ -103,9 +148,9 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    def one_step(seed):
-        bs = solver.solve_blocks(sc.points, W, b0, b1, sc.max_steps, sc.eps, seed=seed)
-        t = solver.last_timing
+    def one_step(seed, slv=solver):
+        bs = slv.solve_blocks(sc.points, W, b0, b1, sc.max_steps, sc.eps, seed=seed)
+        t = slv.last_timing
         full = D.gather_block_stats(bs, nb, device=f"cuda:{local}") if dist is not None else bs   # RCCL all_gather
         return D.point_sums(full, len(sc.points)), t
 
@@ -140,6 +185,12 @@ def main():
         dist.all_reduce(e_max, op=dist.ReduceOp.MAX)
         total_steps = int(s_all[0].item())
         max_elapsed = float(e_max.item())
+
+    # apparent resistivity (second half of the metric), outside the timed region: the
+    # homogeneous-background survey on the same walk streams as the last timed step
+    sc_h = survey.homogeneous(sc, ALPHA_BG)
+    solver_h = sc_h.solver(device=local)
+    sums_h, _ = one_step(args.steps - 1, solver_h)
 
     if rank == 0:
         value = total_steps / max_elapsed
@@ -177,11 +228,23 @@ def main():
                              "algorithmic_bytes_per_launch": bytes_per_launch},
             "u_checksum": float(np.sum(mean)),
         }
+        st_m, st_h = stats_from_sums(sums, W), stats_from_sums(sums_h, W)
+        gpu_full = ((st_m.mean, st_m.stderr), (st_h.mean, st_h.stderr), W)
+        cpu_same = gpu_same = None
+        w_cpu = 0
         if not args.no_cpu and world == 1:
-            out["cpu_baseline"] = cpu_baseline(S.dcr_dipole(n_electrodes=args.electrodes, n_walks=8),
-                                               args.cpu_seconds)
+            base, w_cpu, cm, ch = cpu_leg(sc, sc_h, solver.sigma_bar or 0.0, solver_h.sigma_bar or 0.0,
+                                          args.cpu_seconds)
+            out["cpu_baseline"] = base
+            cpu_same = (cm, ch)
+            _, gm = solver.solve(sc.points, nWalks=w_cpu, maxSteps=sc.max_steps, eps=sc.eps, seed=CPU_SEED,
+                                 return_stats=True)
+            _, gh = solver_h.solve(sc.points, nWalks=w_cpu, maxSteps=sc.max_steps, eps=sc.eps, seed=CPU_SEED,
+                                   return_stats=True)
+            gpu_same = ((gm.mean, gm.stderr), (gh.mean, gh.stderr))
         else:
             out["cpu_baseline"] = None
+        out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -56,7 +56,7 @@ class WostProblem(ctypes.Structure):
 class WostTiming(ctypes.Structure):
     _fields_ = [("walk_kernel_ms", c_double), ("reduce_kernel_ms", c_double), ("total_ms", c_double),
                 ("n_launches", c_int32), ("grid_blocks", c_int32), ("total_steps", c_uint64),
-                ("total_walks", c_uint64), ("jit", c_int32), ("reserved", c_int32)]
+                ("total_walks", c_uint64), ("jit", c_int32), ("tree", c_int32)]
 
 
 class WostError(RuntimeError):
@@ -84,6 +84,7 @@ def _load():
                                  POINTER(c_uint32)]),
         "wost_last_timing": (c_int32, [H, POINTER(WostTiming)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
+        "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
         "wost_eval_field": (c_int32, [H, c_int32, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_sampler_table": (c_int32, [H, POINTER(c_float), c_int32]),
         "wost_geometry_query": (c_int32, [c_int32, c_int32, POINTER(WostPolyline), POINTER(c_float),

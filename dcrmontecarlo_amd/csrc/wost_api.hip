@@ -18,6 +18,7 @@
 #include "wost_internal.h"
 #include "wost_jit.h"
 #include "wost_tables.h"
+#include "wost_tree.h"
 
 using namespace wost;
 
@@ -164,6 +165,14 @@ struct wost_handle {
     uint64_t jit_version = ~0ull;
     std::string jit_error;
 
+    // Neumann segment tree (wost_tree.h): used when the Neumann polyline has at
+    // least tree_min_segments segments (< 0: never)
+    int tree_min_segments = WOST_TREE_MIN_SEGMENTS_DEFAULT;
+    int tree_leaf = WOST_TREE_LEAF_DEFAULT;
+    bool tree_ready = false;
+    SegmentTreeHost tree;
+    float* d_tree = nullptr;
+
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
     float2* d_dverts = nullptr;
@@ -275,12 +284,30 @@ double estimate_sigma_bar(const wost_handle* h, const Program& prog) {
     return sb;
 }
 
+bool use_tree(const wost_handle* h) {
+    const int nseg = (int)(h->nverts.size() / 2) - 1;
+    return nseg >= 1 && h->tree_min_segments >= 0 && nseg >= h->tree_min_segments;
+}
+
 int walk_mode(const wost_handle* h) {
     const bool neu = !h->nverts.empty();
     const bool src = h->fields[SLOT_F].present;
-    if (h->delta) return neu ? MODE_MIXED_DELTA : MODE_DELTA;
-    if (neu) return src ? MODE_MIXED_POISSON : MODE_MIXED;
+    const bool tree = neu && use_tree(h);
+    if (h->delta) return neu ? (tree ? MODE_MIXED_DELTA_TREE : MODE_MIXED_DELTA) : MODE_DELTA;
+    if (neu) return src ? (tree ? MODE_MIXED_POISSON_TREE : MODE_MIXED_POISSON) : (tree ? MODE_MIXED_TREE : MODE_MIXED);
     return src ? MODE_POISSON : MODE_DIRICHLET;
+}
+
+int ensure_tree(wost_handle* h) {
+    if (h->tree_ready) return WOST_OK;
+    if (!build_segment_tree(h->nverts.data(), (int)(h->nverts.size() / 2), h->tree_leaf, &h->tree))
+        return fail(WOST_ERR_INVALID_ARG, "cannot build the Neumann segment tree");
+    if (h->d_tree) (void)hipFree(h->d_tree);
+    h->d_tree = nullptr;
+    HIP_TRY(hipMalloc(&h->d_tree, sizeof(float) * h->tree.node.size()));
+    HIP_TRY(hipMemcpy(h->d_tree, h->tree.node.data(), sizeof(float) * h->tree.node.size(), hipMemcpyHostToDevice));
+    h->tree_ready = true;
+    return WOST_OK;
 }
 
 template <class T>
@@ -352,7 +379,7 @@ void wost_destroy(wost_handle* h) {
     if (!h) return;
     if (h->device >= 0) (void)hipSetDevice(h->device);
     void* ptrs[] = {h->d_dverts, h->d_nverts, h->d_table, h->d_prog, h->d_counter, h->d_val,
-                    h->d_steps, h->d_begin, h->d_bstats, h->d_points};
+                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t& e : h->ev)
@@ -383,6 +410,8 @@ int wost_create(const wost_problem* pb, wost_handle** out) {
     }
     h->compat = pb->compat;
     if (const char* e = std::getenv("WOST_JIT")) h->jit_enabled = std::strcmp(e, "0") != 0;
+    if (const char* e = std::getenv("WOST_TREE_MIN_SEGMENTS")) h->tree_min_segments = std::atoi(e);
+    if (const char* e = std::getenv("WOST_TREE_LEAF")) h->tree_leaf = std::max(1, std::atoi(e));
     // solvers/WoStSolver.py:54-64: any of sigma/alpha turns on delta tracking,
     // the missing one defaults to sigma = 0 / alpha = 1 (constant => Q9 fallback).
     h->delta = h->fields[SLOT_SIGMA].present || h->fields[SLOT_ALPHA].present;
@@ -519,6 +548,7 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     int rc;
     if ((rc = upload_program(h)) != WOST_OK) return rc;
     if (src && (rc = ensure_table(h)) != WOST_OK) return rc;
+    if (mode_tree(mode) && (rc = ensure_tree(h)) != WOST_OK) return rc;
 
     h->timing = wost_timing{};
     const int64_t nblk = block_end - block_begin;
@@ -567,6 +597,12 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     a.key1 = (uint32_t)(seed >> 32);
     a.n_points = (int32_t)std::min<int64_t>(n_points, INT32_MAX);
     a.inv_walks_per_point = 1.0 / (double)W;
+    if (mode_tree(mode)) {
+        a.tree = reinterpret_cast<const float4*>(h->d_tree);
+        a.tree_first_leaf = h->tree.first_leaf;
+        a.tree_leaf = h->tree.leaf;
+        a.tree_tol = h->tree.tol;
+    }
 
     std::vector<int64_t> begins;
     std::vector<float> ms_walk, ms_red;
@@ -653,6 +689,18 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     h->timing.total_steps = steps_sum;
     h->timing.total_walks = (uint64_t)walks_total;
     h->timing.jit = jfn ? 1 : 0;
+    h->timing.tree = mode_tree(mode) ? 1 : 0;
+    return WOST_OK;
+}
+
+int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    if (leaf_segments < 0) return fail(WOST_ERR_INVALID_ARG, "leaf_segments must be >= 0");
+    h->tree_min_segments = min_segments;
+    if (leaf_segments > 0 && leaf_segments != h->tree_leaf) {
+        h->tree_leaf = leaf_segments;
+        h->tree_ready = false;
+    }
     return WOST_OK;
 }
 

@@ -464,6 +464,31 @@ WOST_HD float ray_segment_time_filtered(float2 a, float2 b, float qx, float qy, 
 
 struct Hit { float x, y, nx, ny; bool hit; };
 
+// :179-197 -- the hit (or miss) from the winning segment bi and its "time".
+template <class VP>
+WOST_HD Hit intersect_finish(VP v, int bi, float best, float px, float py, float dx, float dy, float qx, float qy,
+                             float r) {
+#pragma clang fp contract(off)
+    Hit h;
+    if (bi < 0 || best > r || best <= 0.0f) {
+        h.x = px + r * dx; h.y = py + r * dy; h.nx = 0.f; h.ny = 0.f; h.hit = false;
+        return h;
+    }
+    float2 sa = v[bi], sb = v[bi + 1];
+    float ux = sb.x - sa.x, uy = sb.y - sa.y;
+    float len = sqrtf(ux * ux + uy * uy);
+    if (len < 1e-10f) {
+        h.nx = 0.f; h.ny = 1.f;
+    } else {
+        float ex = ux / len, ey = uy / len;
+        h.nx = -ey; h.ny = ex;    // left normal (:191-194)
+    }
+    h.x = qx + best * dx;
+    h.y = qy + best * dy;
+    h.hit = true;
+    return h;
+}
+
 // intersect_polylines_jit (:134-197).
 template <class VP>
 WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, float dyi, float r) {
@@ -485,23 +510,174 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
         if (s < best) { best = s; bi = i - 1; }   // first argmin (:177-178)
         a = b;
     }
-    if (bi < 0 || best > r || best <= 0.0f) {
-        h.x = px + r * dx; h.y = py + r * dy; h.nx = 0.f; h.ny = 0.f; h.hit = false;
+    return intersect_finish(v, bi, best, px, py, dx, dy, qx, qy, r);
+}
+
+// ---------------------------------------------------------------------------
+// Segment tree over a long Neumann polyline (topography with 10^4+ segments).
+// The reference scans every segment at every step (PolylinesSimple.py:83-102,
+// :134-197); these queries return the same bits while visiting only the parts
+// of the polyline that can matter.
+//
+// Implicit complete binary tree (built by wost_api.hip, build_segment_tree):
+// node k has children 2k+1 and 2k+2; leaves are nodes first_leaf.. and leaf l
+// owns segments [l*L, min((l+1)*L, nseg)). A node's range of segments also
+// includes the first segment of its right neighbour (a vertex's silhouette
+// test reads both adjacent segments). node[2k] is the node's bounding box
+// (xmin, ymin, xmax, ymax) of the range's vertices, exact (min/max of vertex
+// coordinates); node[2k+1] is the cone of its segment directions (unit axis,
+// sin and cos of the half-angle; cos < -1.5: no usable cone; sin < -0.5: no
+// segment of non-zero length). Padding leaves have inverted boxes.
+//
+// Exactness:
+//  * the ray query prunes nodes whose box is farther than tol from the ray's
+//    LINE (behind or ahead); a segment the float test accepts lies within a few
+//    ulps of the line (tol is ~2^-14 of the coordinates, 10^3 times that), and
+//    leaves are visited in ascending segment order, so `s < best` keeps the
+//    first argmin like the scan;
+//  * the silhouette query prunes by a box lower bound on the squared distance,
+//    which rounds monotonically (contraction off) to at most any vertex's
+//    computed distance, and by the normal cone: when every segment direction
+//    of the node makes an angle of more than 1e-3 rad with every view vector,
+//    all cross products c1, c2 of :63-81 have one sign and no vertex of the
+//    node is a silhouette. Vertices farther than the Dirichlet distance dd
+//    (+0.2%) cannot change min(dn, dd) (:212), so they are pruned too and the
+//    result is exact for that use.
+// ---------------------------------------------------------------------------
+struct SegTree {
+    const float4* node;   // [2 * n_nodes]
+    const float2* v;      // polyline vertices
+    int nv;               // vertex count
+    int first_leaf;       // index of the first leaf node
+    int leaf;             // segments per leaf
+    float tol;            // line-test tolerance at the origin; grows with |q|
+};
+
+constexpr float kConeMargin = 1e-3f;
+
+WOST_HD int tree_near_child(const SegTree& t, int k, float px, float py) {
+#pragma clang fp contract(off)
+    const float4 a = t.node[2 * (2 * k + 1)], b = t.node[2 * (2 * k + 2)];
+    const float ax = 0.5f * (a.x + a.z) - px, ay = 0.5f * (a.y + a.w) - py;
+    const float bx = 0.5f * (b.x + b.z) - px, by = 0.5f * (b.y + b.w) - py;
+    // an inverted (padding) right child has a NaN centre and is never nearer
+    return (bx * bx + by * by < ax * ax + ay * ay) ? 2 * k + 2 : 2 * k + 1;
+}
+
+// True when no vertex of the node can be a silhouette seen from p.
+WOST_HD bool cone_excludes_silhouettes(float4 box, float4 cone, float px, float py) {
+#pragma clang fp contract(off)
+    if (cone.z < -0.5f) return true;     // only zero-length segments: c1 * c2 == 0
+    if (cone.w < -1.5f) return false;    // directions spread too wide
+    const float hx = 0.5f * (box.z - box.x), hy = 0.5f * (box.w - box.y);
+    const float wx = px - 0.5f * (box.x + box.z), wy = py - 0.5f * (box.y + box.w);
+    const float R2 = hx * hx + hy * hy, D2 = wx * wx + wy * wy;
+    if (!(D2 > R2 * 1.01f)) return false;
+    const float D = sqrtf(D2);
+    const float sw = sqrtf(R2) / D, cw = sqrtf(1.0f - sw * sw);
+    const float sinb = cone.z * cw + cone.w * sw;   // sin(theta_u + theta_w)
+    const float cosb = cone.w * cw - cone.z * sw;
+    if (cosb < 2.0f * kConeMargin) return false;
+    const float cr = cone.x * wy - cone.y * wx;     // D sin(angle(axis, p - centre))
+    return fabsf(cr) > D * (sinb + kConeMargin);
+}
+
+template <class Prune, class Visit>
+WOST_HD void tree_scan(const SegTree& t, Prune prune, Visit visit) {
+    // left-to-right stackless traversal: leaves come in ascending segment order
+    int k = 0;
+    for (;;) {
+        if (!prune(k)) {
+            if (k < t.first_leaf) { k = 2 * k + 1; continue; }
+            visit(k - t.first_leaf);
+        }
+        while (k > 0 && (k & 1) == 0) k = (k - 1) >> 1;   // right child: climb
+        if (k == 0) return;
+        ++k;                                              // left child: its sibling
+    }
+}
+
+// silhouette_distance for the use min(dn, dd) of :212: exact when the result
+// is below dd; otherwise some value >= dd (or +inf).
+WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, float dd) {
+#pragma clang fp contract(off)
+    float best = WOST_INF;
+    const int nv = t.nv, nseg = nv - 1;
+    if (nv < 3) return best;
+    const float T = (dd * dd) * 1.002f;
+    int k = 0;
+    for (;;) {
+        const float4 b = t.node[2 * k];
+        const float gx = fmaxf(fmaxf(b.x - px, px - b.z), 0.0f);
+        const float gy = fmaxf(fmaxf(b.y - py, py - b.w), 0.0f);
+        const float lb = gx * gx + gy * gy;
+        const float bound = best < T ? best : T;
+        bool skip = lb > bound || b.x > b.z;
+        if (!skip) skip = cone_excludes_silhouettes(b, t.node[2 * k + 1], px, py);
+        if (!skip) {
+            if (k < t.first_leaf) { k = tree_near_child(t, k, px, py); continue; }
+            const int s0 = (k - t.first_leaf) * t.leaf;
+            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+            const int j1 = s1 < nv - 2 ? s1 : nv - 2;
+            if (s0 + 1 <= j1) {
+                float2 va = t.v[s0], vb = t.v[s0 + 1];
+                for (int j = s0 + 1; j <= j1; ++j) {
+                    const float2 vc = t.v[j + 1];
+                    if (is_silhouette(va, vb, vc, px, py)) {
+                        const float ex = vb.x - px, ey = vb.y - py;
+                        const float d2 = ex * ex + ey * ey;
+                        best = d2 < best ? d2 : best;
+                    }
+                    va = vb;
+                    vb = vc;
+                }
+            }
+        }
+        // next node: the parent's other child if k was visited first, else climb
+        for (;;) {
+            if (k == 0) return best == WOST_INF ? best : sqrtf(best);
+            const int parent = (k - 1) >> 1;
+            if (k == tree_near_child(t, parent, px, py)) { k = (k & 1) ? k + 1 : k - 1; break; }
+            k = parent;
+        }
+    }
+}
+
+// intersect_polylines over the tree: the same winner as the full scan.
+WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float dxi, float dyi, float r) {
+#pragma clang fp contract(off)
+    Hit h;
+    float dn = sqrtf(dxi * dxi + dyi * dyi);
+    if (dn < 1e-10f) {
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false;
         return h;
     }
-    float2 sa = v[bi], sb = v[bi + 1];
-    float ux = sb.x - sa.x, uy = sb.y - sa.y;
-    float len = sqrtf(ux * ux + uy * uy);
-    if (len < 1e-10f) {
-        h.nx = 0.f; h.ny = 1.f;
-    } else {
-        float ex = ux / len, ey = uy / len;
-        h.nx = -ey; h.ny = ex;    // left normal (:191-194)
-    }
-    h.x = qx + best * dx;
-    h.y = qy + best * dy;
-    h.hit = true;
-    return h;
+    const float dx = dxi / dn, dy = dyi / dn;
+    const float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
+    const float tol = t.tol + 6.103515625e-05f * (fabsf(qx) + fabsf(qy));   // + 2^-14 |q|_1
+    const int nseg = t.nv - 1;
+    float best = WOST_INF;
+    int bi = -1;
+    tree_scan(
+        t,
+        [&](int k) {
+            const float4 b = t.node[2 * k];
+            const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
+            const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
+            return b.x > b.z || fabsf(dx * cy - dy * cx) > fabsf(dx) * hy + fabsf(dy) * hx + tol;
+        },
+        [&](int l) {
+            const int s0 = l * t.leaf;
+            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+            float2 a = t.v[s0];
+            for (int i = s0; i < s1; ++i) {
+                const float2 b = t.v[i + 1];
+                const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
+                if (s < best) { best = s; bi = i; }
+                a = b;
+            }
+        });
+    return intersect_finish(t.v, bi, best, px, py, dx, dy, qx, qy, r);
 }
 
 }  // namespace wost

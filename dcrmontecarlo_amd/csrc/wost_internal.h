@@ -16,15 +16,23 @@ enum WalkMode : int {
     MODE_MIXED = 2,          // + Neumann polyline
     MODE_MIXED_POISSON = 3,  // + Neumann + source
     MODE_DELTA = 4,          // delta tracking (source required), Dirichlet only
-    MODE_MIXED_DELTA = 5     // delta tracking + Neumann
+    MODE_MIXED_DELTA = 5,    // delta tracking + Neumann
+    // the mixed modes with the Neumann queries through the segment tree
+    MODE_MIXED_TREE = 6,
+    MODE_MIXED_POISSON_TREE = 7,
+    MODE_MIXED_DELTA_TREE = 8
 };
 
-inline bool mode_neu(int m) { return m == MODE_MIXED || m == MODE_MIXED_POISSON || m == MODE_MIXED_DELTA; }
-inline bool mode_src(int m) { return m == MODE_POISSON || m == MODE_MIXED_POISSON || m == MODE_DELTA || m == MODE_MIXED_DELTA; }
-inline bool mode_delta(int m) { return m == MODE_DELTA || m == MODE_MIXED_DELTA; }
+inline bool mode_tree(int m) { return m >= MODE_MIXED_TREE && m <= MODE_MIXED_DELTA_TREE; }
+inline bool mode_neu(int m) { return m == MODE_MIXED || m == MODE_MIXED_POISSON || m == MODE_MIXED_DELTA || mode_tree(m); }
+inline bool mode_src(int m) {
+    return m == MODE_POISSON || m == MODE_MIXED_POISSON || m == MODE_DELTA || m == MODE_MIXED_DELTA ||
+           m == MODE_MIXED_POISSON_TREE || m == MODE_MIXED_DELTA_TREE;
+}
+inline bool mode_delta(int m) { return m == MODE_DELTA || m == MODE_MIXED_DELTA || m == MODE_MIXED_DELTA_TREE; }
 
 inline size_t walk_lds_bytes(int mode, int nd, int nn, int n_points) {
-    return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points);
+    return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points, mode_tree(mode));
 }
 
 // precompiled (interpreted-field) walk kernels

@@ -1,5 +1,6 @@
 // wost_jit.cpp -- see wost_jit.h.
 #include "wost_jit.h"
+#include "wost_internal.h"
 
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
@@ -186,9 +187,10 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
 }  // namespace
 
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors) {
-    const bool neu = mode == 2 || mode == 3 || mode == 5;
-    const bool src = mode == 1 || mode == 3 || mode == 4 || mode == 5;
-    const bool delta = mode == 4 || mode == 5;
+    const bool neu = mode_neu(mode);
+    const bool src = mode_src(mode);
+    const bool delta = mode_delta(mode);
+    const bool tree = mode_tree(mode);
     const DField& fG = hdr.field[SLOT_G];
     const DField& fF = hdr.field[SLOT_F];
     const DField& fS = hdr.field[SLOT_SIGMA];
@@ -222,7 +224,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
       << "    const GenFields fld;\n"
       << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
-      << (delta ? "true" : "false") << ">(A, fld, smem);\n}\n";
+      << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ">(A, fld, smem);\n}\n";
     return o.str();
 }
 

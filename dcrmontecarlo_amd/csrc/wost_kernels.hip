@@ -1,6 +1,6 @@
 // wost_kernels.hip -- precompiled gfx950 kernels of the Walk-on-Stars hot path.
 //
-// wost_walk_kernel<NEU,SRC,DELTA>: the walk loop of wost_walk.h with the
+// wost_walk_kernel<NEU,SRC,DELTA,TREE>: the walk loop of wost_walk.h with the
 // coefficient fields interpreted from a program buffer read through the
 // constant address space with uniform indices (scalar loads). wost_jit.cpp
 // builds the same loop with the fields compiled in.
@@ -114,45 +114,44 @@ struct InterpFields {
 // One walk-step of _solveUnified (solvers/WoStSolver.py:206-291) for every
 // active lane, with the finish/refill logic of loops 1-2 (:182-188, :294-311)
 // around it: see wost_walk.h.
-template <bool NEU, bool SRC, bool DELTA>
+template <bool NEU, bool SRC, bool DELTA, bool TREE>
 __global__ void __launch_bounds__(kWalkBlock, WOST_WALK_MIN_WAVES)
 wost_walk_kernel(const WalkArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const InterpFields fld(A.prog);
-    walk_body<NEU, SRC, DELTA>(A, fld, smem);
+    walk_body<NEU, SRC, DELTA, TREE>(A, fld, smem);
 }
+
+// mode -> kernel instantiation (MODE_* of wost_internal.h)
+#define WOST_FOR_MODE(mode, X)                                   \
+    switch (mode) {                                              \
+    case MODE_DIRICHLET: X(false, false, false, false);          \
+    case MODE_POISSON: X(false, true, false, false);             \
+    case MODE_MIXED: X(true, false, false, false);               \
+    case MODE_MIXED_POISSON: X(true, true, false, false);        \
+    case MODE_DELTA: X(false, true, true, false);                \
+    case MODE_MIXED_DELTA: X(true, true, true, false);           \
+    case MODE_MIXED_TREE: X(true, false, false, true);           \
+    case MODE_MIXED_POISSON_TREE: X(true, true, false, true);    \
+    case MODE_MIXED_DELTA_TREE: X(true, true, true, true);       \
+    default: return hipErrorInvalidValue;                        \
+    }
 
 hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu) {
     const size_t lds = walk_lds_bytes(mode, nd, nn, n_points);
-    switch (mode) {
-    case MODE_DIRICHLET:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<false, false, false>, kWalkBlock, lds);
-    case MODE_POISSON:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<false, true, false>, kWalkBlock, lds);
-    case MODE_MIXED:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<true, false, false>, kWalkBlock, lds);
-    case MODE_MIXED_POISSON:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<true, true, false>, kWalkBlock, lds);
-    case MODE_DELTA:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<false, true, true>, kWalkBlock, lds);
-    case MODE_MIXED_DELTA:
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<true, true, true>, kWalkBlock, lds);
-    }
-    return hipErrorInvalidValue;
+#define OCC(n, s, d, t) \
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<n, s, d, t>, kWalkBlock, lds)
+    WOST_FOR_MODE(mode, OCC)
+#undef OCC
 }
 
 hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s) {
     const size_t lds = walk_lds_bytes(mode, a.nd, a.nn, a.n_points);
-    switch (mode) {
-    case MODE_DIRICHLET: wost_walk_kernel<false, false, false><<<grid, kWalkBlock, lds, s>>>(a); break;
-    case MODE_POISSON: wost_walk_kernel<false, true, false><<<grid, kWalkBlock, lds, s>>>(a); break;
-    case MODE_MIXED: wost_walk_kernel<true, false, false><<<grid, kWalkBlock, lds, s>>>(a); break;
-    case MODE_MIXED_POISSON: wost_walk_kernel<true, true, false><<<grid, kWalkBlock, lds, s>>>(a); break;
-    case MODE_DELTA: wost_walk_kernel<false, true, true><<<grid, kWalkBlock, lds, s>>>(a); break;
-    case MODE_MIXED_DELTA: wost_walk_kernel<true, true, true><<<grid, kWalkBlock, lds, s>>>(a); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
+#define LAUNCH(n, sr, d, t)                                                 \
+    wost_walk_kernel<n, sr, d, t><<<grid, kWalkBlock, lds, s>>>(a); \
+    return hipGetLastError()
+    WOST_FOR_MODE(mode, LAUNCH)
+#undef LAUNCH
 }
 
 // ---------------------------------------------------------------------------

@@ -39,6 +39,11 @@ struct WalkArgs {
     int32_t chunk;               // walks claimed per work-queue dequeue
     int32_t n_points;            // query points (staged in LDS when <= kLdsPointsMax)
     double inv_walks_per_point;  // 1/W for the point index of a walk id
+    const float4* tree;          // Neumann segment tree (TREE kernels; wost_device.h SegTree)
+    int32_t tree_first_leaf;
+    int32_t tree_leaf;
+    float tree_tol;
+    int32_t pad_;
 };
 
 constexpr int kWalkBlock = 256;
@@ -46,10 +51,11 @@ constexpr int kLdsPointsMax = 1024;
 
 WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
-// Bytes of dynamic LDS a walk-kernel workgroup needs.
-WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points) {
+// Bytes of dynamic LDS a walk-kernel workgroup needs. With the segment tree
+// the Neumann polyline stays in global memory (read through the caches).
+WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false) {
     size_t b = align16(sizeof(float2) * (size_t)nd);
-    if (neu) b += align16(sizeof(float2) * (size_t)nn);
+    if (neu && !tree) b += align16(sizeof(float2) * (size_t)nn);
     if (src) b += align16(sizeof(float) * WOST_SAMPLER_TABLE_N);
     if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
     return b;
@@ -57,8 +63,8 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 
 // The Fields policy F provides: has_g(), g(x,y), f(x,y), sigma(x,y),
 // alpha(x,y), alpha_jet(x,y), detached(), sigma_bar(), sqrt_sigma_bar(),
-// inv_sigma_bar(), inv_i0(x).
-template <bool NEU, bool SRC, bool DELTA, class F>
+// inv_sigma_bar(), inv_i0(x). TREE: Neumann queries through the segment tree.
+template <bool NEU, bool SRC, bool DELTA, bool TREE, class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
     // the walk's position updates round op by op like the reference (torch CPU
     // has no FMA contraction); the field math it calls keeps its own setting
@@ -66,14 +72,15 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     float2* sD = reinterpret_cast<float2*>(smem);
     float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
     float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
-                                         (NEU ? align16(sizeof(float2) * (size_t)A.nn) : 0));
+                                         ((NEU && !TREE) ? align16(sizeof(float2) * (size_t)A.nn) : 0));
     float2* sP = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(sT) +
                                            (SRC ? align16(sizeof(float) * WOST_SAMPLER_TABLE_N) : 0));
     const bool points_in_lds = A.n_points <= kLdsPointsMax;
 
     for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
-    if (NEU)
+    if (NEU && !TREE)
         for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
+    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_leaf, A.tree_tol};
     if (SRC)
         for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
     if (points_in_lds)
@@ -163,7 +170,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         const float dd = poly_distance(sD, A.nd, px, py);           // :208
         float r;
         if (NEU) {
-            const float dn = silhouette_distance(sN, A.nn, px, py);  // :211
+            const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd)
+                                  : silhouette_distance(sN, A.nn, px, py);  // :211
             const float m = dn < dd ? dn : dd;                       // Python min()
             r = m > A.rmin ? m : A.rmin;                             // Python max() (:212)
         } else {
@@ -178,7 +186,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 
         float xnx, xny;
         if (NEU) {                                                   // :235-236
-            const Hit h = intersect_polylines(sN, A.nn, px, py, cs, sn, r);
+            const Hit h = TREE ? intersect_polylines_tree(tree, px, py, cs, sn, r)
+                               : intersect_polylines(sN, A.nn, px, py, cs, sn, r);
             xnx = h.x; xny = h.y; nx = h.nx; ny = h.ny; onB = h.hit;
         } else {                                                     // :238-239
             xnx = px + r * cs;
@@ -195,7 +204,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             yy = py + rs * sn;
             const float e1x = yx - px, e1y = yy - py;
             const float e2x = xnx - px, e2y = xny - py;
-            clipped = sqrtf(e1x * e1x + e1y * e1y) > sqrtf(e2x * e2x + e2y * e2y);  // :248
+            // :248 compares the two norms. sqrt is monotone, so sqrt(a2) > sqrt(b2)
+            // needs a2 > b2 (rare: only Neumann hits make the next point closer);
+            // only then evaluate the reference's exact comparison.
+            const float a2 = e1x * e1x + e1y * e1y, b2 = e2x * e2x + e2y * e2y;
+            if (a2 > b2) clipped = sqrtf(a2) > sqrtf(b2);
             if (clipped) { yx = xnx; yy = xny; }
             if (DELTA) {
                 gnorm = inv_sb * (1.0f - fld.inv_i0(r * sqrt_sb));   // solvers/utils.py:43-44

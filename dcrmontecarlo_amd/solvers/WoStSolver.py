@@ -194,6 +194,13 @@ class WostSolver_2D:
         kernel that interprets the fields. Both give identical results."""
         _lib.check(_lib.lib.wost_set_jit(self._h, 1 if enable else 0), "wost_set_jit")
 
+    def set_segment_tree(self, min_segments: int = 64, leaf_segments: int = 0):
+        """Route the Neumann closest-silhouette and ray queries through the segment
+        tree when the Neumann polyline has >= min_segments segments (< 0: never,
+        0: always). Results are bit-identical to the full scans."""
+        _lib.check(_lib.lib.wost_set_segment_tree(self._h, int(min_segments), int(leaf_segments)),
+                   "wost_set_segment_tree")
+
     def num_blocks(self, n_points: int, nWalks: int) -> int:
         return int(_lib.lib.wost_num_blocks(int(n_points), int(nWalks)))
 

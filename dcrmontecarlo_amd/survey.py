@@ -1,0 +1,110 @@
+"""DC-resistivity survey layer on top of the Walk-on-Stars solver.
+
+The reference stops at electrode potentials (tests/testGeophysicalScenario.py
+plots u at surface electrodes; the notebook, cells 3 and 21, differences
+adjacent electrodes as a dipole-dipole line and imports SimPEG's
+apparent_resistivity_from_voltage). This module turns potentials into survey
+data:
+
+* electrode arrays: dipole-dipole (receiver M_i = electrode i, N_i = i + 1,
+  notebook cell 3) and Wenner quadripoles (A, M, N, B at spacing a);
+* potential differences dV = u(M) - u(N) with Monte-Carlo standard errors;
+* apparent resistivity rho_a = rho_bg * dV(model) / dV(homogeneous), the
+  homogeneous solve using the background conductivity and the SAME random
+  streams (common random numbers), SURVEY.md 8d;
+* comparisons of two solutions of the same survey (e.g. GPU vs the CPU
+  reference): RMSE of rho_a over resolved dipoles and the MC 1-sigma.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import fields as F
+from .scenarios import Scenario
+
+
+def dipole_dipole_pairs(n_electrodes: int) -> np.ndarray:
+    """[(m, n)] receiver dipoles of adjacent electrodes (notebook cell 3)."""
+    i = np.arange(n_electrodes - 1)
+    return np.stack([i, i + 1], axis=1)
+
+
+def wenner_quadripoles(n_electrodes: int, a: int = 1) -> np.ndarray:
+    """[(A, M, N, B)] Wenner-alpha quadripoles with electrode spacing a (in electrode steps)."""
+    i = np.arange(n_electrodes - 3 * a)
+    return np.stack([i, i + a, i + 2 * a, i + 3 * a], axis=1)
+
+
+@dataclass
+class DipoleData:
+    dv: np.ndarray      # [P] potential differences u(M) - u(N)
+    se: np.ndarray      # [P] their Monte-Carlo standard errors (walks of M and N are independent)
+
+
+def potential_differences(u: np.ndarray, se: np.ndarray, pairs: np.ndarray) -> DipoleData:
+    u = np.asarray(u, np.float64).ravel()
+    se = np.asarray(se, np.float64).ravel()
+    m, n = pairs[:, 0], pairs[:, 1]
+    return DipoleData(u[m] - u[n], np.sqrt(se[m] ** 2 + se[n] ** 2))
+
+
+@dataclass
+class ApparentResistivity:
+    rho_a: np.ndarray     # [P]
+    se: np.ndarray        # [P] delta-method standard error (model and background treated as independent)
+    resolved: np.ndarray  # [P] bool: |dV_homogeneous| > 3 se, where the ratio is meaningful
+
+
+def apparent_resistivity(model: DipoleData, homogeneous: DipoleData, rho_bg: float) -> ApparentResistivity:
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio = model.dv / homogeneous.dv
+        rel = np.sqrt((model.se / model.dv) ** 2 + (homogeneous.se / homogeneous.dv) ** 2)
+    rho = rho_bg * ratio
+    return ApparentResistivity(rho, np.abs(rho) * rel, np.abs(homogeneous.dv) > 3.0 * homogeneous.se)
+
+
+def homogeneous(sc: Scenario, alpha_bg: float) -> Scenario:
+    """The same survey with the conductivity field replaced by its background value."""
+    return Scenario(sc.name + "_homogeneous", sc.dirichlet, sc.neumann, g=sc.g, f=sc.f, sigma=sc.sigma,
+                    alpha=F.const(alpha_bg), points=sc.points, n_walks=sc.n_walks, max_steps=sc.max_steps,
+                    eps=sc.eps, reference=sc.reference)
+
+
+@dataclass
+class SurveyResult:
+    pairs: np.ndarray
+    model: DipoleData
+    background: DipoleData
+    rho: ApparentResistivity
+    u_model: np.ndarray
+    u_background: np.ndarray
+    walk_steps: int
+
+
+def run_dipole_dipole(sc: Scenario, alpha_bg: float, n_walks: int, seed: int = 0, device: int | None = None,
+                      solvers=None) -> SurveyResult:
+    """Solve the survey on the GPU: electrode potentials of the model and of the
+    homogeneous background (same walk streams), then dV and rho_a = (1/alpha_bg) dV/dV_bg."""
+    if solvers is None:
+        solvers = (sc.solver(device=device), homogeneous(sc, alpha_bg).solver(device=device))
+    sm, sh = solvers
+    _, st_m = sm.solve(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=seed, return_stats=True)
+    _, st_h = sh.solve(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=seed, return_stats=True)
+    pairs = dipole_dipole_pairs(len(sc.points))
+    dm = potential_differences(st_m.mean, st_m.stderr, pairs)
+    dh = potential_differences(st_h.mean, st_h.stderr, pairs)
+    return SurveyResult(pairs, dm, dh, apparent_resistivity(dm, dh, 1.0 / alpha_bg), st_m.mean, st_h.mean,
+                        st_m.total_steps + st_h.total_steps)
+
+
+def compare(a: ApparentResistivity, b: ApparentResistivity) -> dict:
+    """RMSE of rho_a between two solutions over dipoles resolved in both, and the
+    RMS of b's Monte-Carlo 1-sigma over the same dipoles (the north-star bound)."""
+    ok = a.resolved & b.resolved & np.isfinite(a.rho_a) & np.isfinite(b.rho_a)
+    if not ok.any():
+        return {"rmse": None, "mc_1sigma": None, "resolved": 0}
+    d = a.rho_a[ok] - b.rho_a[ok]
+    return {"rmse": float(np.sqrt(np.mean(d * d))), "mc_1sigma": float(np.sqrt(np.mean(b.se[ok] ** 2))),
+            "resolved": int(ok.sum())}

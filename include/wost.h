@@ -41,6 +41,10 @@ extern "C" {
 /* Inverse-CDF table resolution of the radial source samplers. */
 #define WOST_SAMPLER_TABLE_N 4097
 
+/* Neumann segment-tree defaults (wost_set_segment_tree). */
+#define WOST_TREE_MIN_SEGMENTS_DEFAULT 64
+#define WOST_TREE_LEAF_DEFAULT 8
+
 enum wost_status {
     WOST_OK = 0,
     WOST_ERR_INVALID_ARG = -1,
@@ -143,7 +147,7 @@ typedef struct {
     uint64_t total_walks;
     int32_t jit;                /* 1: field-specialised (hiprtc) walk kernel,
                                    0: precompiled kernel interpreting the fields */
-    int32_t reserved;
+    int32_t tree;               /* 1: Neumann queries through the segment tree */
 } wost_timing;
 
 int wost_version(void);
@@ -193,6 +197,15 @@ int wost_last_timing(const wost_handle* h, wost_timing* out);
  * interpreting kernel if that fails. enable = 0 forces the precompiled kernel
  * (also: environment WOST_JIT=0). Both give identical results. */
 int wost_set_jit(wost_handle* h, int32_t enable);
+
+/* Neumann segment tree: for a Neumann polyline of at least min_segments
+ * segments (default WOST_TREE_MIN_SEGMENTS_DEFAULT; < 0: never, 0: always)
+ * the walk kernel's closest-silhouette and ray queries (geometry/
+ * PolylinesSimple.py:83-102, :134-197, which scan every segment) go through an
+ * implicit bounding-box / normal-cone tree with leaf_segments segments per
+ * leaf (0 keeps the current value). Results are bit-identical to the scans.
+ * Environment: WOST_TREE_MIN_SEGMENTS, WOST_TREE_LEAF. */
+int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments);
 
 /* Device evaluation of the handle's fields at points (for tests and for the
  * host API): which = 0 g, 1 f, 2 sigma, 3 alpha (value, d/dx, d/dy, Laplacian

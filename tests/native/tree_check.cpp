@@ -1,0 +1,52 @@
+// TEST HARNESS -- host build of the walk kernels' geometry (wost_device.h)
+// comparing the segment-tree queries with the full scans they replace, bit for
+// bit, on caller-supplied queries. Built by tests/test_segment_tree.py.
+#include <cstring>
+#include <vector>
+
+#include "../../dcrmontecarlo_amd/csrc/wost_device.h"
+#include "../../dcrmontecarlo_amd/csrc/wost_tree.h"
+
+using namespace wost;
+
+namespace {
+bool same(float a, float b) {
+    uint32_t x, y;
+    std::memcpy(&x, &a, 4);
+    std::memcpy(&y, &b, 4);
+    return x == y || (a != a && b != b);
+}
+}  // namespace
+
+extern "C" {
+
+// For query i: point pts[i], direction dirs[i] (unnormalised), radius radii[i],
+// Dirichlet distance dd[i]. Counts mismatches of min(silhouette, dd) (:212)
+// into out[0] and of the ray hit (x, y, nx, ny, hit) into out[1]; out[2] =
+// queries with a silhouette closer than dd, out[3] = ray hits (coverage).
+int tree_check(const float* xy, int nv, int leaf, const float* pts, const float* dirs, const float* radii,
+               const float* dd, long n, long* out) {
+    SegmentTreeHost th;
+    if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
+    const SegTree t{reinterpret_cast<const float4*>(th.node.data()), reinterpret_cast<const float2*>(xy), nv,
+                    th.first_leaf, th.leaf, th.tol};
+    const float2* v = reinterpret_cast<const float2*>(xy);
+    out[0] = out[1] = out[2] = out[3] = 0;
+    for (long i = 0; i < n; ++i) {
+        const float px = pts[2 * i], py = pts[2 * i + 1];
+        const float dn_b = silhouette_distance(v, nv, px, py);
+        const float dn_t = silhouette_distance_tree(t, px, py, dd[i]);
+        const float mb = dn_b < dd[i] ? dn_b : dd[i];
+        const float mt = dn_t < dd[i] ? dn_t : dd[i];
+        if (!same(mb, mt)) ++out[0];
+        if (dn_b < dd[i]) ++out[2];
+        const Hit hb = intersect_polylines(v, nv, px, py, dirs[2 * i], dirs[2 * i + 1], radii[i]);
+        const Hit ht = intersect_polylines_tree(t, px, py, dirs[2 * i], dirs[2 * i + 1], radii[i]);
+        if (!same(hb.x, ht.x) || !same(hb.y, ht.y) || !same(hb.nx, ht.nx) || !same(hb.ny, ht.ny) || hb.hit != ht.hit)
+            ++out[1];
+        if (hb.hit) ++out[3];
+    }
+    return 0;
+}
+
+}  // extern "C"

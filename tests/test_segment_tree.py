@@ -1,0 +1,141 @@
+"""The Neumann segment tree returns the same bits as the full scans it replaces.
+
+CPU: the device geometry (wost_device.h, __host__ __device__) is compiled for
+the host together with the tree builder, and fuzzed against the scans of
+geometry/PolylinesSimple.py (silhouetteDistance :83-102 in its use
+min(dn, dD) of solvers/WoStSolver.py:211-212, and intersectPolylines
+:134-197) on random, near-boundary and collinear/near-parallel queries.
+GPU: whole walks with the tree kernels vs the scan kernels, walk for walk.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from dcrmontecarlo_amd import scenarios as S
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("tree") / "libtree_check.so")
+    src = [os.path.join(HERE, "native", "tree_check.cpp"), os.path.join(REPO, "dcrmontecarlo_amd", "csrc", "wost_tree.cpp")]
+    # the geometry is __host__ __device__ HIP: compile it as HIP, call it on the host
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
+                    "-I" + os.path.join(REPO, "include"), "-x", "hip", src[0], "-x", "c++", src[1], "-o", out],
+                   check=True)
+    lib = ctypes.CDLL(out)
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib.tree_check.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, ctypes.c_long,
+                               ctypes.POINTER(ctypes.c_long)]
+    lib.tree_check.restype = ctypes.c_int
+    return lib
+
+
+def run(lib, verts, pts, dirs, radii, dd, leaf=8):
+    f = lambda a: np.ascontiguousarray(a, np.float32)
+    verts, pts, dirs, radii, dd = f(verts), f(pts), f(dirs), f(radii), f(dd)
+    out = (ctypes.c_long * 4)()
+    p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    rc = lib.tree_check(p(verts), verts.shape[0], leaf, p(pts), p(dirs), p(radii), p(dd), pts.shape[0], out)
+    assert rc == 0
+    return list(out)
+
+
+def queries(rng, verts, n):
+    """Mix of domain points, points near the polyline, and rays from the line of
+    a segment along (almost) its direction."""
+    lo, hi = verts.min(0), verts.max(0)
+    span = hi - lo + 1.0
+    k = n // 3
+    a = lo - 0.2 * span + rng.random((k, 2)) * 1.4 * span                       # anywhere
+    i = rng.integers(0, len(verts) - 1, n - k)
+    t = rng.random(n - k)
+    base = verts[i] + t[:, None] * (verts[i + 1] - verts[i])
+    off = rng.normal(size=(n - k, 2)) * 10.0 ** rng.uniform(-6, 1, (n - k, 1))   # near the polyline
+    b = base + off
+    pts = np.concatenate([a, b]).astype(np.float32)
+    th = rng.random(n) * 2 * np.pi
+    dirs = np.stack([np.cos(th), np.sin(th)], 1)
+    # a third of the near points shoot along their segment (collinear / near-parallel)
+    m = n - k
+    sel = k + np.arange(m // 2)
+    u = verts[i[: m // 2] + 1] - verts[i[: m // 2]]
+    rot = rng.normal(size=m // 2) * 10.0 ** rng.uniform(-9, -2, m // 2)
+    c, s = np.cos(rot), np.sin(rot)
+    dirs[sel] = np.stack([u[:, 0] * c - u[:, 1] * s, u[:, 0] * s + u[:, 1] * c], 1) * rng.choice([-1, 1], (m // 2, 1))
+    radii = 10.0 ** rng.uniform(-2, 3, n)
+    dd = 10.0 ** rng.uniform(-1, 3.5, n)
+    dd[rng.random(n) < 0.1] = np.inf
+    return pts, dirs.astype(np.float32), radii, dd
+
+
+@pytest.mark.parametrize("leaf", [1, 3, 8, 32])
+def test_tree_matches_scan_topography(harness, leaf):
+    rng = np.random.default_rng(leaf)
+    verts = S.topography(2000)
+    counts = run(harness, verts, *queries(rng, verts, 60000), leaf=leaf)
+    assert counts[0] == 0 and counts[1] == 0, counts
+    assert counts[2] > 1000 and counts[3] > 1000, counts     # both queries exercised
+
+
+def test_tree_matches_scan_full_topography(harness):
+    rng = np.random.default_rng(7)
+    verts = S.topography(10_000)
+    counts = run(harness, verts, *queries(rng, verts, 60000))
+    assert counts[0] == 0 and counts[1] == 0, counts
+
+
+@pytest.mark.parametrize("shape", ["circle", "zigzag", "random_walk", "degenerate"])
+def test_tree_matches_scan_shapes(harness, shape):
+    rng = np.random.default_rng(["circle", "zigzag", "random_walk", "degenerate"].index(shape))
+    if shape == "circle":                                   # closed, every vertex a silhouette candidate
+        th = np.linspace(0, 2 * np.pi, 513)
+        verts = np.stack([40 * np.cos(th), 40 * np.sin(th)], 1)
+    elif shape == "zigzag":                                 # direction cones too wide to prune
+        x = np.linspace(-50, 50, 801)
+        verts = np.stack([x, np.where(np.arange(801) % 2, 1.0, -1.0)], 1)
+    elif shape == "random_walk":
+        verts = np.cumsum(rng.normal(size=(1500, 2)), 0)
+    else:                                                   # repeated vertices, zero-length segments
+        x = np.repeat(np.linspace(-10, 10, 300), 2)
+        verts = np.stack([x, np.sin(x)], 1)
+    verts = verts.astype(np.float32)
+    counts = run(harness, verts, *queries(rng, verts, 40000))
+    assert counts[0] == 0 and counts[1] == 0, counts
+
+
+def test_tree_small_polylines(harness):
+    rng = np.random.default_rng(3)
+    for nv in (2, 3, 4, 9, 17):
+        verts = rng.normal(size=(nv, 2)).astype(np.float32) * 5
+        counts = run(harness, verts, *queries(rng, verts, 5000))
+        assert counts[0] == 0 and counts[1] == 0, (nv, counts)
+
+
+@pytest.mark.gpu
+def test_gpu_tree_walks_match_scan_walks(gpu_available):
+    """C5-shaped problem (2000-segment topography, reduced): every walk of the tree
+    kernel equals the scan kernel's walk, value and step count, for both the
+    field-specialised and the precompiled kernels."""
+    sc = S.wenner_topography(n_electrodes=16, n_walks=512, n_segments=2000)
+    res = {}
+    for tree in (False, True):
+        for jit in (True, False):
+            s = sc.solver(device=0)
+            s.set_segment_tree(0 if tree else -1)
+            s.set_jit(jit)
+            u, hist = s.solve(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=9,
+                              return_history=True)
+            assert s.last_timing["tree"] == int(tree)
+            v = np.array([w["value"] for i in range(len(sc.points)) for w in hist[i]], np.float32)
+            st = np.array([w["steps"] for i in range(len(sc.points)) for w in hist[i]])
+            res[(tree, jit)] = (v, st)
+    ref = res[(False, True)]
+    for key, (v, st) in res.items():
+        np.testing.assert_array_equal(st, ref[1], err_msg=str(key))
+        np.testing.assert_array_equal(v.view(np.uint32), ref[0].view(np.uint32), err_msg=str(key))

@@ -1,0 +1,94 @@
+"""DCR survey layer: electrode arrays, potential differences, apparent resistivity.
+
+CPU tests cover the host arithmetic (and the oracle's own homogeneous survey);
+the GPU test runs a reduced dcr_dipole survey on the device and compares rho_a
+with the CPU oracle on the same walks (same seeds).
+"""
+import numpy as np
+import pytest
+
+from dcrmontecarlo_amd import scenarios as S
+from dcrmontecarlo_amd import survey
+
+
+def test_dipole_dipole_pairs_adjacent():
+    p = survey.dipole_dipole_pairs(5)
+    assert p.tolist() == [[0, 1], [1, 2], [2, 3], [3, 4]]
+    assert survey.dipole_dipole_pairs(1).shape == (0, 2)
+
+
+def test_wenner_quadripoles():
+    q = survey.wenner_quadripoles(8, a=2)
+    assert q.tolist() == [[0, 2, 4, 6], [1, 3, 5, 7]]
+    assert survey.wenner_quadripoles(3, a=1).shape == (0, 4)
+
+
+def test_potential_differences_and_errors():
+    u = np.array([3.0, 1.0, 0.5])
+    se = np.array([0.3, 0.4, 0.0])
+    d = survey.potential_differences(u, se, survey.dipole_dipole_pairs(3))
+    np.testing.assert_allclose(d.dv, [2.0, 0.5])
+    np.testing.assert_allclose(d.se, [0.5, 0.4])
+
+
+def test_apparent_resistivity_of_background_is_rho_bg():
+    d = survey.DipoleData(np.array([2.0, -1.0, 1e-9]), np.array([0.01, 0.01, 0.01]))
+    r = survey.apparent_resistivity(d, d, 0.01)
+    np.testing.assert_allclose(r.rho_a, 0.01)
+    assert r.resolved.tolist() == [True, True, False]
+
+
+def test_apparent_resistivity_error_propagation():
+    m = survey.DipoleData(np.array([2.0]), np.array([0.2]))
+    h = survey.DipoleData(np.array([1.0]), np.array([0.1]))
+    r = survey.apparent_resistivity(m, h, 0.5)
+    assert r.rho_a[0] == pytest.approx(1.0)
+    assert r.se[0] == pytest.approx(1.0 * np.sqrt(0.1 ** 2 + 0.1 ** 2))
+
+
+def test_compare_uses_jointly_resolved_dipoles():
+    a = survey.ApparentResistivity(np.array([1.0, 2.0, 5.0]), np.array([0.1, 0.1, 0.1]),
+                                   np.array([True, True, False]))
+    b = survey.ApparentResistivity(np.array([1.1, 1.9, 0.0]), np.array([0.2, 0.2, 0.2]),
+                                   np.array([True, True, True]))
+    c = survey.compare(a, b)
+    assert c["resolved"] == 2
+    assert c["rmse"] == pytest.approx(0.1)
+    assert c["mc_1sigma"] == pytest.approx(0.2)
+    none = survey.compare(a, survey.ApparentResistivity(b.rho_a, b.se, np.zeros(3, bool)))
+    assert none == {"rmse": None, "mc_1sigma": None, "resolved": 0}
+
+
+def test_homogeneous_scenario_keeps_survey():
+    sc = S.dcr_dipole(n_electrodes=6, n_walks=10)
+    h = survey.homogeneous(sc, 100.0)
+    assert h.alpha.pack()[0] and h.f is sc.f and h.neumann is sc.neumann
+    np.testing.assert_array_equal(h.points, sc.points)
+    assert float(h.alpha(np.array([1.0, -30.0]))) == pytest.approx(100.0)
+
+
+@pytest.mark.gpu
+def test_gpu_survey_rho_a_matches_cpu_oracle(gpu_available):
+    """Reduced C4 survey (12 electrodes around the sources x 2000 walks): rho_a on
+    the GPU vs the CPU oracle on the same walks. The walks agree one for one up to
+    the scenario's chaos (~1-2% diverge), so the rho_a RMSE is a small fraction of
+    the Monte-Carlo 1-sigma (the north-star bound is RMSE <= 1 sigma)."""
+    from oracle import oracle as O
+
+    sc = S.dcr_dipole(n_electrodes=48, n_walks=2000)
+    sc.points = sc.points[18:30]          # x = -16.5 .. 16.5: around the two sources
+    alpha_bg = 100.0
+    res = survey.run_dipole_dipole(sc, alpha_bg, sc.n_walks, seed=5, device=0)
+    sm, sh = sc.solver(device=0), survey.homogeneous(sc, alpha_bg).solver(device=0)
+    cm = O.Problem.from_scenario(sc, sigma_bar=sm.sigma_bar).solve(sc.points, sc.n_walks, sc.max_steps, sc.eps, 5)
+    ch = O.Problem.from_scenario(survey.homogeneous(sc, alpha_bg), sigma_bar=sh.sigma_bar).solve(
+        sc.points, sc.n_walks, sc.max_steps, sc.eps, 5)
+    pairs = survey.dipole_dipole_pairs(len(sc.points))
+    rc = survey.apparent_resistivity(survey.potential_differences(cm[0], cm[1], pairs),
+                                     survey.potential_differences(ch[0], ch[1], pairs), 1.0 / alpha_bg)
+    c = survey.compare(res.rho, rc)
+    assert c["resolved"] >= 4, c
+    assert c["rmse"] <= 0.5 * c["mc_1sigma"], c
+    # the background survey's own rho_a vs the model's is a different quantity: the
+    # resistive/conductive bodies must move rho_a away from rho_bg somewhere
+    assert np.nanmax(np.abs(res.rho.rho_a[res.rho.resolved] - 0.01)) > 0.0

@@ -16,7 +16,7 @@ from dcrmontecarlo_amd import scenarios as S  # noqa: E402
 SIZES = {
     "laplace_square": (64, 200_000), "manufactured_polynomial": (16, 500_000), "poisson_square": (64, 200_000),
     "variable_coefficients": (256, 20_000), "dcr_dipole": (48, 1_000_000), "notebook_dcr": (21, 200_000),
-    "wenner_topography": (256, 64),
+    "wenner_topography": (256, 2000),
 }
 
 
