@@ -525,9 +525,9 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
 // includes the first segment of its right neighbour (a vertex's silhouette
 // test reads both adjacent segments). node[2k] is the node's bounding box
 // (xmin, ymin, xmax, ymax) of the range's vertices, exact (min/max of vertex
-// coordinates); node[2k+1] is the cone of its segment directions (unit axis,
-// sin and cos of the half-angle; cos < -1.5: no usable cone; sin < -0.5: no
-// segment of non-zero length). Padding leaves have inverted boxes.
+// coordinates); node[2k+1] is the arc of its segment directions as its two
+// edge unit vectors (e1, e2), see cone_excludes_silhouettes. Padding leaves
+// have inverted boxes.
 //
 // Exactness:
 //  * the ray query prunes nodes whose box is farther than tol from the ray's
@@ -537,10 +537,10 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
 //    first argmin like the scan;
 //  * the silhouette query prunes by a box lower bound on the squared distance,
 //    which rounds monotonically (contraction off) to at most any vertex's
-//    computed distance, and by the normal cone: when every segment direction
-//    of the node makes an angle of more than 1e-3 rad with every view vector,
-//    all cross products c1, c2 of :63-81 have one sign and no vertex of the
-//    node is a silhouette. Vertices farther than the Dirichlet distance dd
+//    computed distance, and by the direction cone: when every segment
+//    direction of the node makes an angle of more than ~1e-3 rad with every
+//    view vector, all cross products c1, c2 of :63-81 have one sign and no
+//    vertex of the node is a silhouette. Vertices farther than the Dirichlet distance dd
 //    (+0.2%) cannot change min(dn, dd) (:212), so they are pruned too and the
 //    result is exact for that use.
 // ---------------------------------------------------------------------------
@@ -555,6 +555,13 @@ struct SegTree {
 
 constexpr float kConeMargin = 1e-3f;
 
+#if defined(WOST_TREE_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+extern long g_tree_stats[4];   // host harness only: silhouette nodes, leaves; ray nodes, leaves
+#define WOST_TREE_COUNT(i) (++g_tree_stats[i])
+#else
+#define WOST_TREE_COUNT(i) ((void)0)
+#endif
+
 WOST_HD int tree_near_child(const SegTree& t, int k, float px, float py) {
 #pragma clang fp contract(off)
     const float4 a = t.node[2 * (2 * k + 1)], b = t.node[2 * (2 * k + 2)];
@@ -564,22 +571,33 @@ WOST_HD int tree_near_child(const SegTree& t, int k, float px, float py) {
     return (bx * bx + by * by < ax * ax + ay * ay) ? 2 * k + 2 : 2 * k + 1;
 }
 
-// True when no vertex of the node can be a silhouette seen from p.
+// True when no vertex of the node can be a silhouette seen from p. The cone
+// holds the two edge directions e1, e2 of the arc of the node's segment
+// directions (half-angle < pi/2). For segment u_i from a_i (both in the node),
+// c_i = cross(u_i, p - a_i) of :63-81. Over u in the arc, cross(u, w) is a
+// sinusoid whose minimum magnitude is at an edge; over a_i in the box it is
+// linear in p - a_i, extreme at a corner. So when the 8 values cross(e, p - q)
+// (e = e1, e2; q = box corners) share one sign with margin, every c_i has that
+// sign, c1 * c2 > 0 at every vertex, and none is a silhouette. The margin
+// (1e-3 of |p - q|_1) keeps every c_i far from the float rounding of its
+// evaluation. Codes: e1.x == 2: only zero-length segments (c == 0, never a
+// silhouette); e1.x == 3: directions too spread to prune.
 WOST_HD bool cone_excludes_silhouettes(float4 box, float4 cone, float px, float py) {
 #pragma clang fp contract(off)
-    if (cone.z < -0.5f) return true;     // only zero-length segments: c1 * c2 == 0
-    if (cone.w < -1.5f) return false;    // directions spread too wide
-    const float hx = 0.5f * (box.z - box.x), hy = 0.5f * (box.w - box.y);
-    const float wx = px - 0.5f * (box.x + box.z), wy = py - 0.5f * (box.y + box.w);
-    const float R2 = hx * hx + hy * hy, D2 = wx * wx + wy * wy;
-    if (!(D2 > R2 * 1.01f)) return false;
-    const float D = sqrtf(D2);
-    const float sw = sqrtf(R2) / D, cw = sqrtf(1.0f - sw * sw);
-    const float sinb = cone.z * cw + cone.w * sw;   // sin(theta_u + theta_w)
-    const float cosb = cone.w * cw - cone.z * sw;
-    if (cosb < 2.0f * kConeMargin) return false;
-    const float cr = cone.x * wy - cone.y * wx;     // D sin(angle(axis, p - centre))
-    return fabsf(cr) > D * (sinb + kConeMargin);
+    if (cone.x == 2.0f) return true;
+    if (cone.x == 3.0f) return false;
+    const float wx0 = px - box.x, wx1 = px - box.z;
+    const float wy0 = py - box.y, wy1 = py - box.w;
+    const float mx = fmaxf(fabsf(wx0), fabsf(wx1)), my = fmaxf(fabsf(wy0), fabsf(wy1));
+    const float m = kConeMargin * (mx + my);
+    // cross(e, w) = e.x w.y - e.y w.x at the four corners, for both edges
+    const float a0 = cone.x * wy0, a1 = cone.x * wy1, b0 = cone.y * wx0, b1 = cone.y * wx1;
+    const float c0 = cone.z * wy0, c1 = cone.z * wy1, d0 = cone.w * wx0, d1 = cone.w * wx1;
+    const float v0 = a0 - b0, v1 = a0 - b1, v2 = a1 - b0, v3 = a1 - b1;
+    const float v4 = c0 - d0, v5 = c0 - d1, v6 = c1 - d0, v7 = c1 - d1;
+    const float lo = fminf(fminf(fminf(v0, v1), fminf(v2, v3)), fminf(fminf(v4, v5), fminf(v6, v7)));
+    const float hi = fmaxf(fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)), fmaxf(fmaxf(v4, v5), fmaxf(v6, v7)));
+    return lo > m || hi < -m;
 }
 
 template <class Prune, class Visit>
@@ -607,6 +625,7 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     const float T = (dd * dd) * 1.002f;
     int k = 0;
     for (;;) {
+        WOST_TREE_COUNT(0);
         const float4 b = t.node[2 * k];
         const float gx = fmaxf(fmaxf(b.x - px, px - b.z), 0.0f);
         const float gy = fmaxf(fmaxf(b.y - py, py - b.w), 0.0f);
@@ -616,6 +635,7 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
         if (!skip) skip = cone_excludes_silhouettes(b, t.node[2 * k + 1], px, py);
         if (!skip) {
             if (k < t.first_leaf) { k = tree_near_child(t, k, px, py); continue; }
+            WOST_TREE_COUNT(1);
             const int s0 = (k - t.first_leaf) * t.leaf;
             const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
             const int j1 = s1 < nv - 2 ? s1 : nv - 2;
@@ -661,12 +681,14 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
     tree_scan(
         t,
         [&](int k) {
+            WOST_TREE_COUNT(2);
             const float4 b = t.node[2 * k];
             const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
             const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
             return b.x > b.z || fabsf(dx * cy - dy * cx) > fabsf(dx) * hy + fabsf(dy) * hx + tol;
         },
         [&](int l) {
+            WOST_TREE_COUNT(3);
             const int s0 = l * t.leaf;
             const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
             float2 a = t.v[s0];

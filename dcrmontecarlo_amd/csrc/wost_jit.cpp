@@ -252,6 +252,10 @@ bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, st
     std::vector<char> code;
     const std::string dir = cache_dir();
     const std::string name = std::string("walk_") + arch + "_" + hex + ".hsaco";
+    if (const char* dump = std::getenv("WOST_JIT_DUMP")) {   // generated source, for offline ISA study
+        const std::string s(source);
+        write_file_atomic(dump, std::string("walk_") + hex + ".hip", std::vector<char>(s.begin(), s.end()));
+    }
     if (dir.empty() || !read_file(dir + "/" + name, code)) {
         if (!compile(source, arch, code, err)) return false;
         write_file_atomic(dir, name, code);

@@ -72,7 +72,7 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
         float* cone = box + 4;
         if (lo[k] < 0) {   // padding: inverted box, "no segment" cone
             box[0] = inf; box[1] = inf; box[2] = -inf; box[3] = -inf;
-            cone[0] = 0.f; cone[1] = 0.f; cone[2] = -1.f; cone[3] = 1.f;
+            cone[0] = 2.f; cone[1] = 0.f; cone[2] = 0.f; cone[3] = 0.f;
             continue;
         }
         float xmin = inf, ymin = inf, xmax = -inf, ymax = -inf;
@@ -89,15 +89,15 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
         }
         double axis = 0.0, half = 0.0;
         if (!enclosing_arc(ang, &axis, &half)) {
-            cone[0] = 0.f; cone[1] = 0.f; cone[2] = -1.f; cone[3] = 1.f;
+            cone[0] = 2.f; cone[1] = 0.f; cone[2] = 0.f; cone[3] = 0.f;   // only zero-length segments
         } else if (half >= 0.5 * M_PI - 0.01) {
-            cone[0] = 0.f; cone[1] = 0.f; cone[2] = 0.f; cone[3] = -2.f;   // too wide to prune
+            cone[0] = 3.f; cone[1] = 0.f; cone[2] = 0.f; cone[3] = 0.f;   // too wide to prune
         } else {
-            half += 1e-6;   // cover the float rounding of the stored axis
-            cone[0] = (float)std::cos(axis);
-            cone[1] = (float)std::sin(axis);
-            cone[2] = (float)std::sin(half);
-            cone[3] = (float)std::cos(half);
+            half += 1e-6;   // cover the float rounding of the stored edges
+            cone[0] = (float)std::cos(axis - half);
+            cone[1] = (float)std::sin(axis - half);
+            cone[2] = (float)std::cos(axis + half);
+            cone[3] = (float)std::sin(axis + half);
         }
     }
     return true;

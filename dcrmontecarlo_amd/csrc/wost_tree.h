@@ -8,7 +8,7 @@
 namespace wost {
 
 struct SegmentTreeHost {
-    std::vector<float> node;   // 8 floats per node: box (xmin, ymin, xmax, ymax), cone (ux, uy, sin, cos)
+    std::vector<float> node;   // 8 floats per node: box (xmin, ymin, xmax, ymax), direction-arc edges (e1, e2)
     int first_leaf = 0;        // index of the first leaf node
     int leaf = 0;              // segments per leaf
     float tol = 0.f;           // line-test tolerance at the origin

@@ -4,10 +4,16 @@
 #include <cstring>
 #include <vector>
 
+#define WOST_TREE_STATS 1
+
 #include "../../dcrmontecarlo_amd/csrc/wost_device.h"
 #include "../../dcrmontecarlo_amd/csrc/wost_tree.h"
 
 using namespace wost;
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+long wost::g_tree_stats[4];
+#endif
 
 namespace {
 bool same(float a, float b) {
@@ -19,6 +25,16 @@ bool same(float a, float b) {
 }  // namespace
 
 extern "C" {
+
+// Node / leaf visits of the tree queries since the last call (4 counters).
+void tree_stats(long* out) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    for (int i = 0; i < 4; ++i) {
+        out[i] = g_tree_stats[i];
+        g_tree_stats[i] = 0;
+    }
+#endif
+}
 
 // For query i: point pts[i], direction dirs[i] (unnormalised), radius radii[i],
 // Dirichlet distance dd[i]. Counts mismatches of min(silhouette, dd) (:212)
