@@ -177,6 +177,7 @@ struct wost_handle {
     hipEvent_t ev[6] = {};
     float2* d_dverts = nullptr;
     float2* d_nverts = nullptr;
+    float* d_seg_phi = nullptr;
     float* d_table = nullptr;
     char* d_prog = nullptr;
     size_t d_prog_cap = 0;
@@ -379,7 +380,7 @@ void wost_destroy(wost_handle* h) {
     if (!h) return;
     if (h->device >= 0) (void)hipSetDevice(h->device);
     void* ptrs[] = {h->d_dverts, h->d_nverts, h->d_table, h->d_prog, h->d_counter, h->d_val,
-                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree};
+                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree, h->d_seg_phi};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t& e : h->ev)
@@ -471,6 +472,10 @@ int wost_create(const wost_problem* pb, wost_handle** out) {
     if (!h->nverts.empty()) {
         CREATE_TRY(hipMalloc(&h->d_nverts, sizeof(float) * h->nverts.size()));
         CREATE_TRY(hipMemcpy(h->d_nverts, h->nverts.data(), sizeof(float) * h->nverts.size(), hipMemcpyHostToDevice));
+        const int nseg = (int)(h->nverts.size() / 2) - 1;
+        CREATE_TRY(hipMalloc(&h->d_seg_phi, sizeof(float) * std::max(nseg, 1)));
+        CREATE_TRY(launch_segment_phi(h->d_nverts, nseg, h->d_seg_phi, h->stream));
+        CREATE_TRY(hipStreamSynchronize(h->stream));
     }
 #undef CREATE_TRY
     if ((rc = upload_program(h)) != WOST_OK) {
@@ -584,6 +589,7 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     a.points = h->d_points;
     a.dverts = h->d_dverts;
     a.nverts = h->d_nverts;
+    a.seg_phi = h->d_seg_phi;
     a.table = h->d_table;
     a.prog = h->d_prog;
     a.counter = h->d_counter;

@@ -462,41 +462,52 @@ WOST_HD float ray_segment_time_filtered(float2 a, float2 b, float qx, float qy, 
     return res;
 }
 
-struct Hit { float x, y, nx, ny; bool hit; };
+struct Hit { float x, y, nx, ny; bool hit; int seg; };
+
+// Left unit normal of segment a->b (PolylinesSimple.py:189-194): (0, 1) for a
+// degenerate segment.
+WOST_HD float2 segment_left_normal(float2 sa, float2 sb) {
+#pragma clang fp contract(off)
+    float ux = sb.x - sa.x, uy = sb.y - sa.y;
+    float len = sqrtf(ux * ux + uy * uy);
+    if (len < 1e-10f) return float2{0.f, 1.f};
+    float ex = ux / len, ey = uy / len;
+    return float2{-ey, ex};
+}
 
 // :179-197 -- the hit (or miss) from the winning segment bi and its "time".
-template <class VP>
+// NORMAL = false leaves the normal out (the walk kernels look up the
+// segment's precomputed normal angle by h.seg instead).
+template <bool NORMAL = true, class VP>
 WOST_HD Hit intersect_finish(VP v, int bi, float best, float px, float py, float dx, float dy, float qx, float qy,
                              float r) {
 #pragma clang fp contract(off)
     Hit h;
     if (bi < 0 || best > r || best <= 0.0f) {
-        h.x = px + r * dx; h.y = py + r * dy; h.nx = 0.f; h.ny = 0.f; h.hit = false;
+        h.x = px + r * dx; h.y = py + r * dy; h.nx = 0.f; h.ny = 0.f; h.hit = false; h.seg = -1;
         return h;
     }
-    float2 sa = v[bi], sb = v[bi + 1];
-    float ux = sb.x - sa.x, uy = sb.y - sa.y;
-    float len = sqrtf(ux * ux + uy * uy);
-    if (len < 1e-10f) {
-        h.nx = 0.f; h.ny = 1.f;
+    if (NORMAL) {
+        const float2 n = segment_left_normal(v[bi], v[bi + 1]);
+        h.nx = n.x; h.ny = n.y;
     } else {
-        float ex = ux / len, ey = uy / len;
-        h.nx = -ey; h.ny = ex;    // left normal (:191-194)
+        h.nx = 0.f; h.ny = 0.f;
     }
     h.x = qx + best * dx;
     h.y = qy + best * dy;
     h.hit = true;
+    h.seg = bi;
     return h;
 }
 
 // intersect_polylines_jit (:134-197).
-template <class VP>
+template <bool NORMAL = true, class VP>
 WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
     Hit h;
     float dn = sqrtf(dxi * dxi + dyi * dyi);
     if (dn < 1e-10f) {
-        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false;
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
         return h;
     }
     float dx = dxi / dn, dy = dyi / dn;
@@ -510,7 +521,7 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
         if (s < best) { best = s; bi = i - 1; }   // first argmin (:177-178)
         a = b;
     }
-    return intersect_finish(v, bi, best, px, py, dx, dy, qx, qy, r);
+    return intersect_finish<NORMAL>(v, bi, best, px, py, dx, dy, qx, qy, r);
 }
 
 // ---------------------------------------------------------------------------
@@ -664,12 +675,13 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
 }
 
 // intersect_polylines over the tree: the same winner as the full scan.
+template <bool NORMAL = true>
 WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
     Hit h;
     float dn = sqrtf(dxi * dxi + dyi * dyi);
     if (dn < 1e-10f) {
-        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false;
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
         return h;
     }
     const float dx = dxi / dn, dy = dyi / dn;
@@ -699,7 +711,7 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
                 a = b;
             }
         });
-    return intersect_finish(t.v, bi, best, px, py, dx, dy, qx, qy, r);
+    return intersect_finish<NORMAL>(t.v, bi, best, px, py, dx, dy, qx, qy, r);
 }
 
 }  // namespace wost

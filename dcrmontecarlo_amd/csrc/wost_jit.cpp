@@ -6,6 +6,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -219,7 +220,9 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "};\n        const float cb[" << kChebB << "] = {";
     for (int k = 0; k < kChebB; ++k) o << (k ? ", " : "") << lit(hdr.cheb_b[k]);
     o << "};\n        return wost::inv_i0(ca, cb, x);\n    }\n};\n}  // namespace\n\n";
-    o << "extern \"C\" __global__ void __launch_bounds__(wost::kWalkBlock, 6)\n"
+    int waves = 6;   // waves per SIMD the register budget is sized for (tools/ab_bench.sh)
+    if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
+    o << "extern \"C\" __global__ void __launch_bounds__(wost::kWalkBlock, " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
       << "    const GenFields fld;\n"

@@ -39,6 +39,7 @@ struct WalkArgs {
     int32_t chunk;               // walks claimed per work-queue dequeue
     int32_t n_points;            // query points (staged in LDS when <= kLdsPointsMax)
     double inv_walks_per_point;  // 1/W for the point index of a walk id
+    const float* seg_phi;        // [nn-1] atan2 of each Neumann segment's left normal
     const float4* tree;          // Neumann segment tree (TREE kernels; wost_device.h SegTree)
     int32_t tree_first_leaf;
     int32_t tree_leaf;
@@ -55,7 +56,7 @@ WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 // the Neumann polyline stays in global memory (read through the caches).
 WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false) {
     size_t b = align16(sizeof(float2) * (size_t)nd);
-    if (neu && !tree) b += align16(sizeof(float2) * (size_t)nn);
+    if (neu && !tree) b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
     if (src) b += align16(sizeof(float) * WOST_SAMPLER_TABLE_N);
     if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
     return b;
@@ -71,15 +72,19 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #pragma clang fp contract(off)
     float2* sD = reinterpret_cast<float2*>(smem);
     float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
-    float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
-                                         ((NEU && !TREE) ? align16(sizeof(float2) * (size_t)A.nn) : 0));
+    float* sPhi = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
+                                           ((NEU && !TREE) ? align16(sizeof(float2) * (size_t)A.nn) : 0));
+    float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sPhi) +
+                                         ((NEU && !TREE) ? align16(sizeof(float) * (size_t)(A.nn > 1 ? A.nn - 1 : 0)) : 0));
     float2* sP = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(sT) +
                                            (SRC ? align16(sizeof(float) * WOST_SAMPLER_TABLE_N) : 0));
     const bool points_in_lds = A.n_points <= kLdsPointsMax;
 
     for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
-    if (NEU && !TREE)
+    if (NEU && !TREE) {
         for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
+        for (int i = threadIdx.x; i < A.nn - 1; i += blockDim.x) sPhi[i] = A.seg_phi[i];
+    }
     const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_leaf, A.tree_tol};
     if (SRC)
         for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
@@ -106,7 +111,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     float dD = 1.0f;            // dDirichlet seeded with 1.0 (:190, quirk Q12)
     int k = 0;                  // step_count
     bool onB = false;           // onBoundary
-    float nx = 0.f, ny = 1.f;   // normal
+    float phi = 0.f;            // atan2 of currentNormal (:228), set when onB
     float w = 1.f;              // attenuation_coef
     float ax = 1.f;             // alpha(current_point), cached
     float total = 0.f;          // this walk's contributions
@@ -154,7 +159,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 if (points_in_lds) q = sP[pid];
                 else q = A.points[pid];
                 px = q.x; py = q.y;
-                k = 0; dD = 1.0f; onB = false; nx = 0.f; ny = 1.f; w = 1.f; total = 0.f;
+                k = 0; dD = 1.0f; onB = false; phi = 0.f; w = 1.f; total = 0.f;
                 if (DELTA) ax = fld.alpha(px, py);
                 active = true;
             }
@@ -181,14 +186,17 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         const U4 rn = philox4x32_10(U4{(uint32_t)k, 0u, (uint32_t)wid, (uint32_t)(wid >> 32)},
                                     A.key0, A.key1);
         float theta = (u01(rn.x) * 2.0f) * kPiF;                     // :226
-        if (NEU && onB) theta = theta / 2.0f + atan2f(ny, nx);       // :227-228 (quirk Q2)
+        // :227-228 (quirk Q2): atan2(normal) is a property of the segment that
+        // was hit, precomputed per segment with the same device atan2f
+        if (NEU && onB) theta = theta / 2.0f + phi;
         const float cs = f_cos(theta), sn = f_sin(theta);            // :230-232
 
         float xnx, xny;
         if (NEU) {                                                   // :235-236
-            const Hit h = TREE ? intersect_polylines_tree(tree, px, py, cs, sn, r)
-                               : intersect_polylines(sN, A.nn, px, py, cs, sn, r);
-            xnx = h.x; xny = h.y; nx = h.nx; ny = h.ny; onB = h.hit;
+            const Hit h = TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
+                               : intersect_polylines<false>(sN, A.nn, px, py, cs, sn, r);
+            xnx = h.x; xny = h.y; onB = h.hit;
+            if (h.hit) phi = TREE ? A.seg_phi[h.seg] : sPhi[h.seg];
         } else {                                                     // :238-239
             xnx = px + r * cs;
             xny = py + r * sn;

@@ -44,8 +44,15 @@ def _field_cost(field, jet: bool) -> float:
     return total
 
 
-def flops_per_step(scenario) -> float:
-    """Model FLOPs of one walk-step of the scenario's kernel variant."""
+TREE_MIN_SEGMENTS = 64       # include/wost.h WOST_TREE_MIN_SEGMENTS_DEFAULT
+
+
+def flops_per_step(scenario):
+    """Model FLOPs of one walk-step of the scenario's kernel variant, or None when
+    the Neumann queries go through the segment tree: its work depends on the
+    traversal, and the reference's full-scan count would exceed the peak."""
+    if scenario.neumann is not None and scenario.neumann.shape[0] - 1 >= TREE_MIN_SEGMENTS:
+        return None
     nd = scenario.dirichlet.shape[0]
     F = 23.0 * (nd - 1) + 1.0
     neu = scenario.neumann is not None

@@ -194,7 +194,7 @@ class WostSolver_2D:
         kernel that interprets the fields. Both give identical results."""
         _lib.check(_lib.lib.wost_set_jit(self._h, 1 if enable else 0), "wost_set_jit")
 
-    def set_segment_tree(self, min_segments: int = 32, leaf_segments: int = 0):
+    def set_segment_tree(self, min_segments: int = 64, leaf_segments: int = 0):
         """Route the Neumann closest-silhouette and ray queries through the segment
         tree when the Neumann polyline has >= min_segments segments (< 0: never,
         0: always). Results are bit-identical to the full scans."""

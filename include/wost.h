@@ -42,7 +42,7 @@ extern "C" {
 #define WOST_SAMPLER_TABLE_N 4097
 
 /* Neumann segment-tree defaults (wost_set_segment_tree). */
-#define WOST_TREE_MIN_SEGMENTS_DEFAULT 32
+#define WOST_TREE_MIN_SEGMENTS_DEFAULT 64
 #define WOST_TREE_LEAF_DEFAULT 8
 
 enum wost_status {

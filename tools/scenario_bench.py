@@ -48,7 +48,7 @@ def main():
         fps = perfmodel.flops_per_step(sc)
         best["steps_per_s_kernel"] = best["steps"] / (best["kernel_ms"] * 1e-3)
         best["steps_per_s_wall"] = best["steps"] / best["wall_s"]
-        best["model_tflops"] = fps * best["steps_per_s_kernel"] / 1e12
+        best["model_tflops"] = fps * best["steps_per_s_kernel"] / 1e12 if fps else float("nan")
         best["frac_fp32"] = best["model_tflops"] / perfmodel.FP32_PEAK_TFLOPS
         best["mean_steps"] = best["steps"] / (npts * W)
         best["config"] = f"{npts} pts x {W} walks"
