@@ -221,7 +221,8 @@ hipFunction_t jit_kernel(wost_handle* h, int mode) {
     h->jit_fn = nullptr;
     h->jit_mode = mode;
     h->jit_version = h->prog_version;
-    const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors());
+    const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2));
     std::string err;
     hipFunction_t fn = nullptr;
     if (!jit_get_kernel(h->device, src, &fn, &err)) {

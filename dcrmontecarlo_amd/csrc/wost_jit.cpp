@@ -187,7 +187,8 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
 
 }  // namespace
 
-std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors) {
+std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
+                         const float* dverts, int nd, const float* nverts, int nn) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -219,7 +220,35 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     for (int k = 0; k < kChebA; ++k) o << (k ? ", " : "") << lit(hdr.cheb_a[k]);
     o << "};\n        const float cb[" << kChebB << "] = {";
     for (int k = 0; k < kChebB; ++k) o << (k ? ", " : "") << lit(hdr.cheb_b[k]);
-    o << "};\n        return wost::inv_i0(ca, cb, x);\n    }\n};\n}  // namespace\n\n";
+    o << "};\n        return wost::inv_i0(ca, cb, x);\n    }\n";
+    // a short Dirichlet polyline is compiled in: the scan unrolls, the segment
+    // vectors and squared lengths fold to constants (the same IEEE operations)
+    o << "    __device__ __forceinline__ float dirichlet_distance(const float2* sD, int nd, float x, float y) const {\n";
+    if (nd <= kJitMaxConstVertices) {
+        o << "        const float2 v[" << nd << "] = {";
+        for (int i = 0; i < nd; ++i) o << (i ? ", " : "") << "{" << lit(dverts[2 * i]) << ", " << lit(dverts[2 * i + 1]) << "}";
+        o << "};\n        return wost::poly_distance(v, " << nd << ", x, y);\n";
+    } else {
+        o << "        return wost::poly_distance(sD, nd, x, y);\n";
+    }
+    o << "    }\n";
+    const bool nconst = neu && !tree && nn >= 1 && nn <= kJitMaxConstVertices;
+    auto nverts_decl = [&]() {
+        std::ostringstream v;
+        v << "        const float2 v[" << nn << "] = {";
+        for (int i = 0; i < nn; ++i) v << (i ? ", " : "") << "{" << lit(nverts[2 * i]) << ", " << lit(nverts[2 * i + 1]) << "}";
+        v << "};\n";
+        return v.str();
+    };
+    o << "    __device__ __forceinline__ float neumann_silhouette_distance(const float2* sN, int nn, float x, float y) const {\n";
+    if (nconst) o << nverts_decl() << "        return wost::silhouette_distance(v, " << nn << ", x, y);\n";
+    else o << "        return wost::silhouette_distance(sN, nn, x, y);\n";
+    o << "    }\n";
+    o << "    __device__ __forceinline__ wost::Hit neumann_intersect(const float2* sN, int nn, float x, float y, float dx,"
+         " float dy, float r) const {\n";
+    if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
+    else o << "        return wost::intersect_polylines<false>(sN, nn, x, y, dx, dy, r);\n";
+    o << "    }\n};\n}  // namespace\n\n";
     int waves = 6;   // waves per SIMD the register budget is sized for (tools/ab_bench.sh)
     if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
     o << "extern \"C\" __global__ void __launch_bounds__(wost::kWalkBlock, " << waves << ")\n"

@@ -18,9 +18,15 @@
 
 namespace wost {
 
+// Polylines of at most this many vertices are compiled into the specialised
+// kernel as constants.
+constexpr int kJitMaxConstVertices = 16;
+
 // HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
-// (wost_internal.h WalkMode) with the fields of `prog` compiled in.
-std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors);
+// (wost_internal.h WalkMode) with the fields of `prog` and short polylines
+// (Dirichlet dverts[2*nd], Neumann nverts[2*nn]) compiled in.
+std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
+                         const float* dverts, int nd, const float* nverts, int nn);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

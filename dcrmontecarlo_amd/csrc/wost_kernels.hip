@@ -105,6 +105,16 @@ struct InterpFields {
     __device__ __forceinline__ float sqrt_sigma_bar() const { return sqsb; }
     __device__ __forceinline__ float inv_sigma_bar() const { return isb; }
     __device__ __forceinline__ float inv_i0(float x) const { return wost::inv_i0(ca, cb, x); }
+    __device__ __forceinline__ float dirichlet_distance(const float2* sD, int nd, float x, float y) const {
+        return poly_distance(sD, nd, x, y);
+    }
+    __device__ __forceinline__ float neumann_silhouette_distance(const float2* sN, int nn, float x, float y) const {
+        return silhouette_distance(sN, nn, x, y);
+    }
+    __device__ __forceinline__ Hit neumann_intersect(const float2* sN, int nn, float x, float y, float dx, float dy,
+                                                     float r) const {
+        return intersect_polylines<false>(sN, nn, x, y, dx, dy, r);
+    }
 };
 
 #ifndef WOST_WALK_MIN_WAVES

@@ -64,7 +64,11 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 
 // The Fields policy F provides: has_g(), g(x,y), f(x,y), sigma(x,y),
 // alpha(x,y), alpha_jet(x,y), detached(), sigma_bar(), sqrt_sigma_bar(),
-// inv_sigma_bar(), inv_i0(x). TREE: Neumann queries through the segment tree.
+// inv_sigma_bar(), inv_i0(x), and the polyline scans dirichlet_distance(sD,
+// nd, x, y), neumann_silhouette_distance(sN, nn, x, y), neumann_intersect(sN,
+// nn, x, y, dx, dy, r) (the interpreted kernels scan the staged vertices; the
+// specialised ones may have them compiled in). TREE: Neumann queries through
+// the segment tree.
 template <bool NEU, bool SRC, bool DELTA, bool TREE, class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
     // the walk's position updates round op by op like the reference (torch CPU
@@ -172,11 +176,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         if (!(active && (k < A.max_steps) && (dD > A.eps))) continue;
 
         // --- one walk-step (:206-291)
-        const float dd = poly_distance(sD, A.nd, px, py);           // :208
+        const float dd = fld.dirichlet_distance(sD, A.nd, px, py);  // :208
         float r;
         if (NEU) {
             const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd)
-                                  : silhouette_distance(sN, A.nn, px, py);  // :211
+                                  : fld.neumann_silhouette_distance(sN, A.nn, px, py);  // :211
             const float m = dn < dd ? dn : dd;                       // Python min()
             r = m > A.rmin ? m : A.rmin;                             // Python max() (:212)
         } else {
@@ -194,7 +198,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float xnx, xny;
         if (NEU) {                                                   // :235-236
             const Hit h = TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
-                               : intersect_polylines<false>(sN, A.nn, px, py, cs, sn, r);
+                               : fld.neumann_intersect(sN, A.nn, px, py, cs, sn, r);
             xnx = h.x; xny = h.y; onB = h.hit;
             if (h.hit) phi = TREE ? A.seg_phi[h.seg] : sPhi[h.seg];
         } else {                                                     // :238-239
