@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--electrodes", type=int, default=48)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-rho", action="store_true", help="skip the apparent-resistivity leg (profiling runs)")
     return ap.parse_args()
 
 
@@ -189,8 +190,10 @@ def main():
     # apparent resistivity (second half of the metric), outside the timed region: the
     # homogeneous-background survey on the same walk streams as the last timed step
     sc_h = survey.homogeneous(sc, ALPHA_BG)
-    solver_h = sc_h.solver(device=local)
-    sums_h, _ = one_step(args.steps - 1, solver_h)
+    solver_h = sums_h = None
+    if not args.no_rho:
+        solver_h = sc_h.solver(device=local)
+        sums_h, _ = one_step(args.steps - 1, solver_h)
 
     if rank == 0:
         value = total_steps / max_elapsed
@@ -228,11 +231,11 @@ def main():
                              "algorithmic_bytes_per_launch": bytes_per_launch},
             "u_checksum": float(np.sum(mean)),
         }
-        st_m, st_h = stats_from_sums(sums, W), stats_from_sums(sums_h, W)
-        gpu_full = ((st_m.mean, st_m.stderr), (st_h.mean, st_h.stderr), W)
         cpu_same = gpu_same = None
         w_cpu = 0
         if not args.no_cpu and world == 1:
+            if solver_h is None:
+                solver_h = sc_h.solver(device=local)
             base, w_cpu, cm, ch = cpu_leg(sc, sc_h, solver.sigma_bar or 0.0, solver_h.sigma_bar or 0.0,
                                           args.cpu_seconds)
             out["cpu_baseline"] = base
@@ -244,7 +247,10 @@ def main():
             gpu_same = ((gm.mean, gm.stderr), (gh.mean, gh.stderr))
         else:
             out["cpu_baseline"] = None
-        out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu)
+        if not args.no_rho:
+            st_m, st_h = stats_from_sums(sums, W), stats_from_sums(sums_h, W)
+            gpu_full = ((st_m.mean, st_m.stderr), (st_h.mean, st_h.stderr), W)
+            out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
