@@ -85,6 +85,7 @@ def _load():
         "wost_last_timing": (c_int32, [H, POINTER(WostTiming)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
+        "wost_kernel_source": (c_int32, [POINTER(WostProblem), ctypes.c_char_p, c_int64, POINTER(c_int64)]),
         "wost_eval_field": (c_int32, [H, c_int32, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_sampler_table": (c_int32, [H, POINTER(c_float), c_int32]),
         "wost_geometry_query": (c_int32, [c_int32, c_int32, POINTER(WostPolyline), POINTER(c_float),

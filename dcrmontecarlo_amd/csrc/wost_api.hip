@@ -390,8 +390,13 @@ void wost_destroy(wost_handle* h) {
     delete h;
 }
 
-int wost_create(const wost_problem* pb, wost_handle** out) {
-    if (!pb || !out) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+}  // extern "C"
+
+namespace {
+
+// The host half of wost_create: validation, field conversion, sigma_bar. No
+// HIP call; the handle's device is -1 until wost_create takes a device.
+int create_host(const wost_problem* pb, wost_handle** out) {
     *out = nullptr;
     if (pb->compat != WOST_COMPAT_REFERENCE) {
         if (pb->compat == WOST_COMPAT_FIXED)
@@ -436,12 +441,26 @@ int wost_create(const wost_problem* pb, wost_handle** out) {
             build_program(h->fields, 1.0, tmp);
             h->sigma_bar = estimate_sigma_bar(h, tmp);
             if (!(h->sigma_bar > 0.0)) {
-                wost_destroy(h);
+                delete h;
                 return fail(WOST_ERR_INVALID_ARG,
                             "sigma' could not be evaluated at any grid point (reference raises ValueError, utils.py:108-109)");
             }
         }
     }
+    *out = h;
+    return WOST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wost_create(const wost_problem* pb, wost_handle** out) {
+    if (!pb || !out) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    wost_handle* h = nullptr;
+    int rc = create_host(pb, &h);
+    if (rc != WOST_OK) return rc;
+    *out = nullptr;
 
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
@@ -697,6 +716,25 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     h->timing.total_walks = (uint64_t)walks_total;
     h->timing.jit = jfn ? 1 : 0;
     h->timing.tree = mode_tree(mode) ? 1 : 0;
+    return WOST_OK;
+}
+
+int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int64_t* length) {
+    if (!pb || !length) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    wost_handle* h = nullptr;
+    int rc = create_host(pb, &h);
+    if (rc != WOST_OK) return rc;
+    build_program(h->fields, h->sigma_bar, h->prog);
+    const int mode = walk_mode(h);
+    const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2));
+    delete h;
+    *length = (int64_t)src.size();
+    if (out && capacity > 0) {
+        const size_t n = std::min<size_t>(src.size(), (size_t)capacity - 1);
+        std::memcpy(out, src.data(), n);
+        out[n] = '\0';
+    }
     return WOST_OK;
 }
 

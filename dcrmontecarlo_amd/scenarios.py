@@ -40,6 +40,15 @@ class Scenario:
                              PolyLinesSimple(self.neumann) if self.neumann is not None else None,
                              source=self.f, sigma=self.sigma, alpha=self.alpha, **kw)
 
+    def kernel_source(self, **kw) -> str:
+        """Generated source of this scenario's field-specialised walk kernel (host only)."""
+        from .geometry import PolyLinesSimple
+        from .solvers.WoStSolver import kernel_source
+
+        return kernel_source(PolyLinesSimple(self.dirichlet), self.g,
+                             PolyLinesSimple(self.neumann) if self.neumann is not None else None,
+                             source=self.f, sigma=self.sigma, alpha=self.alpha, **kw)
+
 
 def torch_linspace(start: float, end: float, steps: int) -> np.ndarray:
     """torch.linspace in float32 (ATen CPU: first half from start, second half from end)."""

@@ -75,6 +75,42 @@ def stats_from_sums(sums: np.ndarray, n_walks: int, total_steps=None, kernel_ms=
                       kernel_ms=float(kernel_ms), total_ms=float(total_ms))
 
 
+def _problem(dxy, nxy, g, f, sigma, alpha, compat, device, sigma_bar):
+    """wost_problem for the given geometry and fields (None = absent; the library
+    applies the sigma = 0 / alpha = 1 defaults itself) and the objects to keep alive."""
+    keep = []
+    dpoly, k1 = _lib.make_polyline(dxy)
+    npoly, k2 = _lib.make_polyline(nxy)
+    fields = {}
+    for name, fld in (("boundary", g), ("source", f), ("sigma", sigma), ("alpha", alpha)):
+        wf, k = _lib.make_field(fld)
+        fields[name] = ctypes.pointer(wf) if wf is not None else None
+        keep.append(k)
+    prob = _lib.WostProblem(dpoly, npoly, fields["boundary"], fields["source"], fields["sigma"], fields["alpha"],
+                            _lib.COMPAT[compat], int(device), float(sigma_bar) if sigma_bar else 0.0)
+    return prob, keep + [k1, k2]
+
+
+def kernel_source(dirichletBoundary, dirichletBoundaryFunction=None, neumannBoundary=None, source=None,
+                  sigma=None, alpha=None, *, sigma_bar: float | None = None) -> str:
+    """HIP source of the field-specialised walk kernel a WostSolver_2D with these
+    arguments would compile (no device needed; wost_kernel_source)."""
+    dxy = np.asarray(_np(dirichletBoundary.points), dtype=np.float32).reshape(-1, 2)
+    nxy = None if neumannBoundary is None else np.asarray(_np(neumannBoundary.points), dtype=np.float32).reshape(-1, 2)
+    g = _field_or_none(dirichletBoundaryFunction, "dirichletBoundaryFunction")
+    f = _field_or_none(source, "source")
+    s = _field_or_none(sigma, "sigma")
+    a = _field_or_none(alpha, "alpha")
+    if a is not None and a.is_constant():
+        a = detach(a)
+    prob, keep = _problem(dxy, nxy, g, f, s, a, "reference", 0, sigma_bar)
+    n = ctypes.c_int64(0)
+    _lib.check(_lib.lib.wost_kernel_source(ctypes.byref(prob), None, 0, ctypes.byref(n)), "wost_kernel_source")
+    buf = ctypes.create_string_buffer(n.value + 1)
+    _lib.check(_lib.lib.wost_kernel_source(ctypes.byref(prob), buf, n.value + 1, ctypes.byref(n)), "wost_kernel_source")
+    return buf.value.decode()
+
+
 class WostSolver_2D:
     """Walk-on-Stars solver for -div(alpha grad u) + sigma u = f with Dirichlet
     and (optionally) Neumann polyline boundaries, on a HIP device."""
@@ -109,23 +145,12 @@ class WostSolver_2D:
             device = int(os.environ.get("WOST_DEVICE", os.environ.get("LOCAL_RANK", "0")))
         self.device = int(device)
 
-        self._keep = []
-        dpoly, k1 = _lib.make_polyline(dxy)
-        npoly, k2 = _lib.make_polyline(nxy)
-        fields = {}
-        # the library applies the sigma = 0 / alpha = 1 defaults itself
-        for name, f in (("boundary", self.boundaryDirichlet), ("source", self.source),
-                        ("sigma", self.sigma if sigma is not None else None),
-                        ("alpha", self.alpha if alpha is not None else None)):
-            wf, keep = _lib.make_field(f)
-            fields[name] = ctypes.pointer(wf) if wf is not None else None
-            self._keep.append(keep)
-        prob = _lib.WostProblem(dpoly, npoly, fields["boundary"], fields["source"], fields["sigma"], fields["alpha"],
-                                _lib.COMPAT[compat], self.device, float(sigma_bar) if sigma_bar else 0.0)
+        prob, self._keep = _problem(dxy, nxy, self.boundaryDirichlet, self.source,
+                                    self.sigma if sigma is not None else None,
+                                    self.alpha if alpha is not None else None, compat, self.device, sigma_bar)
         h = ctypes.c_void_p()
         _lib.check(_lib.lib.wost_create(ctypes.byref(prob), ctypes.byref(h)), "WostSolver_2D")
         self._h = h
-        self._keep += [k1, k2]
         sb = ctypes.c_double(0.0)
         dt = ctypes.c_int32(0)
         _lib.check(_lib.lib.wost_get_info(self._h, ctypes.byref(sb), ctypes.byref(dt)), "wost_get_info")

@@ -207,6 +207,14 @@ int wost_set_jit(wost_handle* h, int32_t enable);
  * Environment: WOST_TREE_MIN_SEGMENTS, WOST_TREE_LEAF. */
 int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments);
 
+/* HIP source of the field-specialised walk kernel wost_create would build for
+ * this problem (host only, no device needed): for offline ISA study and for
+ * checking on a build machine that the generator's output compiles.
+ * *length = source length; the source (NUL-terminated, truncated to
+ * capacity - 1) is copied to out when out != NULL. Compile it against
+ * wost.h, dcrmontecarlo_amd/csrc/wost_device.h and wost_walk.h. */
+int wost_kernel_source(const wost_problem* problem, char* out, int64_t capacity, int64_t* length);
+
 /* Device evaluation of the handle's fields at points (for tests and for the
  * host API): which = 0 g, 1 f, 2 sigma, 3 alpha (value, d/dx, d/dy, Laplacian
  * per point -> out[n][4]), 4 sigma' (solvers/WoStSolver.py:88-127 -> out[n][4],
