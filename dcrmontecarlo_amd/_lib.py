@@ -82,6 +82,8 @@ def _load():
         "wost_solve": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
                                  c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_float),
                                  POINTER(c_uint32)]),
+        "wost_solve_history": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int32, c_float, c_uint64,
+                                         POINTER(c_double), POINTER(c_float), POINTER(c_uint32), POINTER(c_float)]),
         "wost_last_timing": (c_int32, [H, POINTER(WostTiming)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
@@ -169,3 +171,5 @@ def declared_symbols() -> list[str]:
     hdr = os.path.join(here, "include", "wost.h")
     text = open(hdr).read()
     return sorted(set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(wost_\w+)\s*\(", text, re.M)))
+
+REC_FLOATS = 8   # include/wost.h WOST_REC_FLOATS

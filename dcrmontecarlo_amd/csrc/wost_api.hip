@@ -213,16 +213,19 @@ int upload_program(wost_handle* h) {
     return WOST_OK;
 }
 
-// The field-specialised kernel for `mode`, or nullptr when it is disabled or
-// could not be built (the precompiled kernel is used then; same results).
-hipFunction_t jit_kernel(wost_handle* h, int mode) {
+// The field-specialised kernel for `mode` (with the walk recorder compiled in
+// when `record`), or nullptr when it is disabled or could not be built (the
+// precompiled kernel is used then; same results).
+hipFunction_t jit_kernel(wost_handle* h, int mode, bool record) {
     if (!h->jit_enabled) return nullptr;
-    if (h->jit_mode == mode && h->jit_version == h->prog_version) return h->jit_fn;
+    const int key = 2 * mode + (record ? 1 : 0);
+    if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
-    h->jit_mode = mode;
+    h->jit_mode = key;
     h->jit_version = h->prog_version;
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
-                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2));
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2),
+                                         record);
     std::string err;
     hipFunction_t fn = nullptr;
     if (!jit_get_kernel(h->device, src, &fn, &err)) {
@@ -545,9 +548,17 @@ int wost_last_timing(const wost_handle* h, wost_timing* out) {
     return WOST_OK;
 }
 
-int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
-               int64_t block_begin, int64_t block_end, int32_t max_steps, float eps, uint64_t seed,
-               double* block_stats, double* point_stats, float* walk_values, uint32_t* walk_steps) {
+}  // extern "C"
+
+namespace {
+
+constexpr int64_t kMaxRecordBatchBytes = int64_t(1) << 30;   // device buffer of the walk recorder
+
+// wost_solve, and with `records` != null also the walk recorder
+// (wost_solve_history): records[walk][max_steps + 1][kRecFloats] on the host.
+int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W, int64_t block_begin,
+               int64_t block_end, int32_t max_steps, float eps, uint64_t seed, double* block_stats,
+               double* point_stats, float* walk_values, uint32_t* walk_steps, float* records) {
     if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
     if (n_points < 0 || (n_points > 0 && !points)) return fail(WOST_ERR_INVALID_ARG, "bad points");
     if (W <= 0) return fail(WOST_ERR_INVALID_ARG, "nWalks must be >= 1 (got %lld)", (long long)W);
@@ -588,12 +599,29 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     };
 
     const int64_t walks_total = blk_end(block_end - 1) - blk_begin(block_begin);
+    // walks per launch: the recorder's device buffer bounds it
+    int64_t batch_limit = kMaxBatchWalks;
+    const int64_t rec_stride = (int64_t)max_steps + 1;
+    const int64_t rec_walk_bytes = rec_stride * kRecFloats * (int64_t)sizeof(float);
+    if (records) {
+        batch_limit = std::min<int64_t>(kMaxBatchWalks, kMaxRecordBatchBytes / rec_walk_bytes);
+        if (batch_limit < std::min<int64_t>(W, WOST_BLOCK_WALKS))
+            return fail(WOST_ERR_INVALID_ARG,
+                        "return_history: %lld recorded steps per walk need more than %lld bytes per walk block; "
+                        "lower maxSteps or nWalks", (long long)rec_stride, (long long)kMaxRecordBatchBytes);
+    }
     if ((rc = ensure_cap(h->d_points, h->points_cap, std::max<int64_t>(n_points, 1))) != WOST_OK) return rc;
     HIP_TRY(hipMemcpyAsync(h->d_points, points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
-    if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, kMaxBatchWalks))) != WOST_OK) return rc;
+    if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, batch_limit))) != WOST_OK) return rc;
     if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * 3)) != WOST_OK) return rc;
+    float* d_rec = nullptr;
+    struct RecFree {
+        float*& p;
+        ~RecFree() { if (p) (void)hipFree(p); }
+    } rec_free{d_rec};
+    if (records) HIP_TRY(hipMalloc(&d_rec, (size_t)std::min<int64_t>(walks_total, batch_limit) * rec_walk_bytes));
 
-    const hipFunction_t jfn = jit_kernel(h, mode);
+    const hipFunction_t jfn = jit_kernel(h, mode, records != nullptr);
     const size_t lds = walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points);
     int blocks_per_cu = 0;
     if (jfn)
@@ -623,6 +651,8 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     a.key1 = (uint32_t)(seed >> 32);
     a.n_points = (int32_t)std::min<int64_t>(n_points, INT32_MAX);
     a.inv_walks_per_point = 1.0 / (double)W;
+    a.rec = d_rec;
+    a.rec_stride = (int32_t)rec_stride;
     if (mode_tree(mode)) {
         a.tree = reinterpret_cast<const float4*>(h->d_tree);
         a.tree_first_leaf = h->tree.first_leaf;
@@ -642,7 +672,7 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         const int64_t wb = blk_begin(j);
         int64_t j2 = j;
         begins.clear();
-        while (j2 < block_end && blk_end(j2) - wb <= kMaxBatchWalks) {
+        while (j2 < block_end && blk_end(j2) - wb <= batch_limit) {
             begins.push_back(blk_begin(j2) - wb);
             ++j2;
         }
@@ -680,6 +710,9 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
             HIP_TRY(hipMemcpyAsync(walk_values + walks_done, h->d_val, sizeof(float) * count, hipMemcpyDeviceToHost, h->stream));
         if (walk_steps)
             HIP_TRY(hipMemcpyAsync(walk_steps + walks_done, h->d_steps, sizeof(uint32_t) * count, hipMemcpyDeviceToHost, h->stream));
+        if (records)
+            HIP_TRY(hipMemcpyAsync(records + walks_done * rec_stride * kRecFloats, d_rec, (size_t)count * rec_walk_bytes,
+                                   hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipEventSynchronize(h->ev[2]));
         float t0 = 0.f, t1 = 0.f;
         HIP_TRY(hipEventElapsedTime(&t0, h->ev[0], h->ev[1]));
@@ -719,6 +752,27 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     return WOST_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
+               int64_t block_begin, int64_t block_end, int32_t max_steps, float eps, uint64_t seed,
+               double* block_stats, double* point_stats, float* walk_values, uint32_t* walk_steps) {
+    return solve_impl(h, points, n_points, W, block_begin, block_end, max_steps, eps, seed, block_stats,
+                      point_stats, walk_values, walk_steps, nullptr);
+}
+
+int wost_solve_history(wost_handle* h, const float* points, int64_t n_points, int64_t W, int32_t max_steps,
+                       float eps, uint64_t seed, double* point_stats, float* walk_values, uint32_t* walk_steps,
+                       float* records) {
+    if (!records) return fail(WOST_ERR_INVALID_ARG, "NULL records");
+    const int64_t nb = wost_num_blocks(n_points, W);
+    return solve_impl(h, points, n_points, W, 0, nb, max_steps, eps, seed, nullptr, point_stats, walk_values,
+                      walk_steps, records);
+}
+
+
 int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int64_t* length) {
     if (!pb || !length) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
     wost_handle* h = nullptr;
@@ -727,7 +781,8 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
     build_program(h->fields, h->sigma_bar, h->prog);
     const int mode = walk_mode(h);
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
-                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2));
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2),
+                                         false);
     delete h;
     *length = (int64_t)src.size();
     if (out && capacity > 0) {

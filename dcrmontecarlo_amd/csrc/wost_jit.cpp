@@ -188,7 +188,7 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
 }  // namespace
 
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
-                         const float* dverts, int nd, const float* nverts, int nn) {
+                         const float* dverts, int nd, const float* nverts, int nn, bool record) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -256,7 +256,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
       << "    const GenFields fld;\n"
       << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
-      << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ">(A, fld, smem);\n}\n";
+      << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
+      << ">(A, fld, smem);\n}\n";
     return o.str();
 }
 

@@ -24,9 +24,10 @@ constexpr int kJitMaxConstVertices = 16;
 
 // HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
 // (wost_internal.h WalkMode) with the fields of `prog` and short polylines
-// (Dirichlet dverts[2*nd], Neumann nverts[2*nn]) compiled in.
+// (Dirichlet dverts[2*nd], Neumann nverts[2*nn]) compiled in; `record`: the
+// kernel can record walks (return_history).
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
-                         const float* dverts, int nd, const float* nverts, int nn);
+                         const float* dverts, int nd, const float* nverts, int nn, bool record);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

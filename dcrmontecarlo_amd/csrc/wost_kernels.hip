@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(kWalkBlock, WOST_WALK_MIN_WAVES)
 wost_walk_kernel(const WalkArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const InterpFields fld(A.prog);
-    walk_body<NEU, SRC, DELTA, TREE>(A, fld, smem);
+    walk_body<NEU, SRC, DELTA, TREE, true>(A, fld, smem);   // records when A.rec is set
 }
 
 // mode -> kernel instantiation (MODE_* of wost_internal.h)

@@ -40,6 +40,9 @@ struct WalkArgs {
     int32_t n_points;            // query points (staged in LDS when <= kLdsPointsMax)
     double inv_walks_per_point;  // 1/W for the point index of a walk id
     const float* seg_phi;        // [nn-1] atan2 of each Neumann segment's left normal
+    float* rec;                  // walk recorder (return_history), or null: kRecFloats floats per
+                                 // record, rec_stride records per local walk
+    int32_t rec_stride;          // max_steps + 1
     const float4* tree;          // Neumann segment tree (TREE kernels; wost_device.h SegTree)
     int32_t tree_first_leaf;
     int32_t tree_leaf;
@@ -48,6 +51,15 @@ struct WalkArgs {
 };
 
 constexpr int kWalkBlock = 256;
+
+// Walk recorder (solvers/WoStSolver.py:197-309, return_history). Record k < steps
+// of a walk is its step k: the pre-step point and its distances (:218-222), the
+// source sample point after clipping and its contribution (:261-266).
+// Record `steps` is the end: final point (REC_X, REC_Y), boundary contribution
+// (REC_C) and the walk's total (REC_AUX) (:301-306). A step record's REC_AUX is
+// 1 when the step sampled the source.
+constexpr int kRecFloats = WOST_REC_FLOATS;   // include/wost.h, wost_solve_history
+enum RecField { REC_X = 0, REC_Y, REC_DD, REC_DN, REC_SX, REC_SY, REC_C, REC_AUX };
 constexpr int kLdsPointsMax = 1024;
 
 WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -68,8 +80,8 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // nd, x, y), neumann_silhouette_distance(sN, nn, x, y), neumann_intersect(sN,
 // nn, x, y, dx, dy, r) (the interpreted kernels scan the staged vertices; the
 // specialised ones may have them compiled in). TREE: Neumann queries through
-// the segment tree.
-template <bool NEU, bool SRC, bool DELTA, bool TREE, class F>
+// the segment tree. REC: the kernel can record walks (A.rec).
+template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
     // the walk's position updates round op by op like the reference (torch CPU
     // has no FMA contraction); the field math it calls keeps its own setting
@@ -127,6 +139,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             if (DELTA) g = g * w;
             total = total + g;
             const int64_t li = (int64_t)(wid - (uint64_t)A.wid_begin);
+            if (REC && A.rec != nullptr) {
+                float* rr = A.rec + ((size_t)li * (size_t)A.rec_stride + (size_t)k) * kRecFloats;
+                rr[REC_X] = px; rr[REC_Y] = py; rr[REC_C] = g; rr[REC_AUX] = total;   // end record
+            }
             A.out_val[li] = total;
             A.out_steps[li] = (uint32_t)k;
             active = false;
@@ -178,9 +194,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         // --- one walk-step (:206-291)
         const float dd = fld.dirichlet_distance(sD, A.nd, px, py);  // :208
         float r;
+        float dnv = WOST_NAN;                                        // recorder: None without Neumann
         if (NEU) {
             const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd)
                                   : fld.neumann_silhouette_distance(sN, A.nn, px, py);  // :211
+            dnv = dn;
             const float m = dn < dd ? dn : dd;                       // Python min()
             r = m > A.rmin ? m : A.rmin;                             // Python max() (:212)
         } else {
@@ -207,6 +225,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         }
 
         float yx = xnx, yy = xny;
+        float cv = 0.0f;                                             // recorder: source contribution
         bool clipped = false;
         float gnorm = 0.f;
         Jet aj{0.f, 0.f, 0.f, 0.f};
@@ -235,6 +254,15 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                     c = f * ((r * r) / 4.0f);                        // :256, utils.py:61
             }
             total = total + c;                                       // :258
+            cv = c;
+        }
+        if (REC && A.rec != nullptr) {                               // :218-222, :261-266
+            // the tree's silhouette distance is exact only below dD: recompute it
+            if (TREE) dnv = silhouette_distance_tree(tree, px, py, WOST_INF);
+            const int64_t li = (int64_t)(wid - (uint64_t)A.wid_begin);
+            float4* rr = reinterpret_cast<float4*>(A.rec + ((size_t)li * (size_t)A.rec_stride + (size_t)k) * kRecFloats);
+            rr[0] = float4{px, py, dd, dnv};
+            rr[1] = float4{yx, yy, cv, SRC ? 1.0f : 0.0f};
         }
 
         if (DELTA) {                                                 // :271-284

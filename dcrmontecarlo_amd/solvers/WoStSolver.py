@@ -239,11 +239,14 @@ class WostSolver_2D:
         """Estimate u at each point (reference: solvers/WoStSolver.py:319-353).
 
         Returns ``[N, 1]`` float32 (torch tensor if ``solvePoints`` is one). With
-        ``return_history=True`` returns ``(u, history)`` where history has the
-        reference's per-point list of walk dicts (``walk_id``,
-        ``total_contribution`` as the running point total like :308, plus this
-        walk's ``value`` and ``steps``; paths are not recorded). With
-        ``return_stats=True`` a :class:`SolveStats` is appended.
+        ``return_history=True`` returns ``(u, history)`` with the reference's
+        structure (:335-350): per point a list of walk dicts with ``walk_id``,
+        ``path`` (each step's point and Dirichlet / Neumann distances),
+        ``contributions`` (each step's source sample and contribution, then the
+        boundary term) and ``total_contribution`` (the running point total, :308),
+        plus this walk's ``value`` and ``steps``. Points are torch tensors when
+        ``solvePoints`` is one, numpy arrays otherwise. With ``return_stats=True``
+        a :class:`SolveStats` is appended.
         """
         p = _points_np(solvePoints)
         n = p.shape[0]
@@ -251,30 +254,80 @@ class WostSolver_2D:
         if nWalks < 1:
             raise ValueError("nWalks must be >= 1")
         sums = np.zeros((n, 3), np.float64)
-        wv = ws = None
         if return_history:
             wv = np.empty(n * nWalks, np.float32)
             ws = np.empty(n * nWalks, np.uint32)
-        nb = self.num_blocks(n, nWalks)
-        _lib.check(_lib.lib.wost_solve(self._h, _lib.fptr(p), n, nWalks, 0, nb, int(maxSteps), float(eps),
-                                       int(seed) & (2**64 - 1), None, _lib.dptr(sums), _lib.fptr(wv), _lib.u32ptr(ws)),
-                   "WostSolver_2D.solve")
+            stride = int(maxSteps) + 1
+            rec = np.empty((n * nWalks, stride, _lib.REC_FLOATS), np.float32)
+            _lib.check(_lib.lib.wost_solve_history(self._h, _lib.fptr(p), n, nWalks, int(maxSteps), float(eps),
+                                                   int(seed) & (2**64 - 1), _lib.dptr(sums), _lib.fptr(wv),
+                                                   _lib.u32ptr(ws), _lib.fptr(rec)),
+                       "WostSolver_2D.solve")
+        else:
+            nb = self.num_blocks(n, nWalks)
+            _lib.check(_lib.lib.wost_solve(self._h, _lib.fptr(p), n, nWalks, 0, nb, int(maxSteps), float(eps),
+                                           int(seed) & (2**64 - 1), None, _lib.dptr(sums), None, None),
+                       "WostSolver_2D.solve")
         self.last_timing = self.timing()
         u = (sums[:, 0] / nWalks).astype(np.float32).reshape(n, 1)
         out = [_like(u, solvePoints)]
         if return_history:
-            hist = {}
-            for i in range(n):
-                vals = wv[i * nWalks:(i + 1) * nWalks]
-                run = np.cumsum(vals.astype(np.float64))
-                hist[i] = [{"walk_id": j, "path": [], "contributions": [], "value": float(vals[j]),
-                            "steps": int(ws[i * nWalks + j]), "total_contribution": float(run[j])}
-                           for j in range(nWalks)]
-            out.append(hist)
+            out.append(_history(rec, wv, ws, n, nWalks, self.neumannBoundary is not None, self.source is not None,
+                                _is_torch(solvePoints)))
         if return_stats:
             t = self.last_timing
             out.append(stats_from_sums(sums, nWalks, t["total_steps"], t["walk_kernel_ms"], t["total_ms"]))
         return out[0] if len(out) == 1 else tuple(out)
+
+    def solve_walks(self, solvePoints, nWalks=1000, maxSteps=1000, eps=1e-4, *, seed: int = 0):
+        """Per-walk results without the paths: (values float32 [N, nWalks],
+        steps uint32 [N, nWalks]) in walk order (walk j of point i has global id
+        i * nWalks + j, as in return_history)."""
+        p = _points_np(solvePoints)
+        n = p.shape[0]
+        nWalks = int(nWalks)
+        if nWalks < 1:
+            raise ValueError("nWalks must be >= 1")
+        wv = np.empty(n * nWalks, np.float32)
+        ws = np.empty(n * nWalks, np.uint32)
+        nb = self.num_blocks(n, nWalks)
+        _lib.check(_lib.lib.wost_solve(self._h, _lib.fptr(p), n, nWalks, 0, nb, int(maxSteps), float(eps),
+                                       int(seed) & (2**64 - 1), None, None, _lib.fptr(wv), _lib.u32ptr(ws)),
+                   "WostSolver_2D.solve_walks")
+        self.last_timing = self.timing()
+        return wv.reshape(n, nWalks), ws.reshape(n, nWalks)
+
+
+def _history(rec, wv, ws, n, nWalks, has_neumann, has_source, as_torch):
+    """The reference's history_dict (solvers/WoStSolver.py:180-309) from the recorder's
+    records (include/wost.h, wost_solve_history)."""
+    if as_torch:
+        import torch
+
+        pt = lambda x, y: torch.tensor([float(x), float(y)], dtype=torch.float32)
+    else:
+        pt = lambda x, y: np.array([x, y], np.float32)
+    hist = {}
+    for i in range(n):
+        walks = []
+        running = 0.0
+        for j in range(nWalks):
+            g = i * nWalks + j
+            k = int(ws[g])
+            r = rec[g]
+            path = [{"point": pt(r[s, 0], r[s, 1]), "dirichlet_distance": float(r[s, 2]),
+                     "neumann_distance": float(r[s, 3]) if has_neumann else None} for s in range(k)]
+            contrib = []
+            if has_source:
+                contrib = [{"step": s, "type": "source", "point": pt(r[s, 4], r[s, 5]), "contribution": float(r[s, 6])}
+                           for s in range(k)]
+            contrib.append({"step": k, "type": "boundary", "point": pt(r[k, 0], r[k, 1]),
+                            "contribution": float(r[k, 6])})
+            running += float(wv[g])
+            walks.append({"walk_id": j, "path": path, "contributions": contrib, "total_contribution": running,
+                          "value": float(wv[g]), "steps": k})
+        hist[i] = walks
+    return hist
 
 
 def _np(a):

@@ -189,6 +189,26 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points,
                double* block_stats, double* point_stats,
                float* walk_values, uint32_t* walk_steps);
 
+/* _solveUnified with return_history=True (solvers/WoStSolver.py:180-314): a
+ * full solve (all walks of all points) that also records every walk.
+ * records (host, caller-owned): [n_points * walks_per_point][max_steps + 1]
+ * [WOST_REC_FLOATS] floats, walk-major in walk order. Record k < steps of a
+ * walk is its step k:
+ *   x, y      the point at the start of the step        (path 'point', :219)
+ *   dD, dN    its Dirichlet / Neumann distance; dN = NaN without a Neumann
+ *             polyline                                 (:220-221)
+ *   sx, sy    the source sample point after clipping    (contributions 'point', :264)
+ *   c         its source contribution (0 when clipped)  (:265)
+ *   src       1 when the problem has a source (the step has a contribution)
+ * Record `steps` (the walk's step count) is the end of the walk: x, y = final
+ * point, c = boundary contribution g*w, src (slot 7) = the walk's total
+ * (:301-306). The recorder's device buffer is bounded (1 GiB per launch);
+ * solves whose single walk block does not fit fail with WOST_ERR_INVALID_ARG. */
+#define WOST_REC_FLOATS 8
+int wost_solve_history(wost_handle* h, const float* points, int64_t n_points,
+                       int64_t walks_per_point, int32_t max_steps, float eps, uint64_t seed,
+                       double* point_stats, float* walk_values, uint32_t* walk_steps, float* records);
+
 int wost_last_timing(const wost_handle* h, wost_timing* out);
 
 /* Walk kernels: by default libwost compiles a field-specialised walk kernel per

@@ -145,6 +145,93 @@ def test_replay_reference_walks(gpu_available, name):
     np.testing.assert_allclose(u.ravel(), z["u"], rtol=1e-4, atol=1e-6 * scale)
 
 
+@pytest.mark.parametrize("name", SCEN)
+def test_replay_reference_histories(gpu_available, name):
+    """return_history against the reference's own history_dict on the same Philox
+    stream (tests/golden/replay_*.npz, path_* / src_* / boundary_values): every
+    step's point and Dirichlet/Neumann distances, every source sample point and
+    contribution, the boundary terms and the running totals. A walk counts as
+    matching when all its records agree (2e-3 relative for positions and
+    distances, 1e-4 for contributions); >= 99% must (the chaotic
+    variable-coefficient scenario: its measured floor, 97%; one walk of a
+    sample smaller than 100)."""
+    z = golden(f"replay_{name}.npz")
+    sc, s = _solver_for(name, z)
+    W = int(z["n_walks"])
+    pts = z["points"]
+    u, hist = s.solve(pts, nWalks=W, maxSteps=int(z["max_steps"]), eps=float(z["eps"]), seed=int(z["seed"]),
+                      return_history=True)
+    walks = [w for i in range(len(pts)) for w in hist[i]]
+    steps = z["walk_steps"]
+    assert [w["steps"] for w in walks] == list(steps)
+    assert all(len(w["path"]) == w["steps"] for w in walks)
+    has_src = z["src_points"].shape[0] > 0
+    off = np.concatenate([[0], np.cumsum(steps)])
+    # positions may drift by float rounding over hundreds of steps (Neumann hits
+    # feed 1-ulp differences back into the walk): 2e-3 relative, the scale of the
+    # per-walk value agreement of test_device_matches_oracle
+    tol = lambda a, b: np.all(np.abs(a - b) <= 2e-3 * (1.0 + np.abs(b)))
+    ok = []
+    for j, w in enumerate(walks):
+        a, b = off[j], off[j + 1]
+        P = np.array([np.asarray(st["point"], np.float32) for st in w["path"]]).reshape(-1, 2)
+        dd = np.array([st["dirichlet_distance"] for st in w["path"]], np.float32)
+        dn = np.array([np.nan if st["neumann_distance"] is None else st["neumann_distance"] for st in w["path"]],
+                      np.float32)
+        good = tol(P, z["path_points"][a:b]) and tol(dd, z["path_dd"][a:b])
+        rdn = z["path_dn"][a:b]
+        good = good and np.array_equal(np.isnan(dn), np.isnan(rdn)) and np.array_equal(np.isinf(dn), np.isinf(rdn))
+        fin = np.isfinite(rdn)
+        good = good and tol(dn[fin], rdn[fin])
+        src = [c for c in w["contributions"] if c["type"] == "source"]
+        bnd = w["contributions"][-1]
+        assert bnd["type"] == "boundary" and bnd["step"] == w["steps"]
+        if has_src:
+            assert len(src) == w["steps"]
+            SP = np.array([np.asarray(c["point"], np.float32) for c in src]).reshape(-1, 2)
+            SV = np.array([c["contribution"] for c in src], np.float32)
+            scale = max(float(np.abs(z["src_values"]).max()), 1e-30)
+            good = good and tol(SP, z["src_points"][a:b])
+            good = good and np.all(np.abs(SV - z["src_values"][a:b]) <= 1e-4 * np.abs(z["src_values"][a:b]) + 1e-6 * scale)
+        else:
+            assert not src
+        good = good and tol(np.asarray(bnd["point"], np.float32), z["final_points"][j])
+        # g vanishes near the boundary of the manufactured problems: an absolute floor
+        # at the walk values' scale, like the per-walk value test above
+        vscale = max(float(np.abs(z["walk_values"]).max()), 1e-30)
+        good = good and abs(bnd["contribution"] - z["boundary_values"][j]) <= 1e-4 * abs(z["boundary_values"][j]) + 1e-6 * vscale
+        ok.append(bool(good))
+    ok = np.array(ok)
+    from test_oracle_golden import AGREEMENT_FLOOR   # the scenario's measured chaos (1-ulp sensitivity)
+    floor = min(0.99, AGREEMENT_FLOOR.get(name, 0.99), 1.0 - 1.0 / len(ok))   # small samples: one walk
+    assert ok.mean() >= floor, f"{(~ok).sum()} of {len(ok)} walks differ"
+    # running point totals (:308) follow from the per-walk values
+    tot = np.array([w["total_contribution"] for w in walks])
+    vals = np.array([w["value"] for w in walks], np.float64)
+    for i in range(len(pts)):
+        np.testing.assert_allclose(tot[i * W:(i + 1) * W], np.cumsum(vals[i * W:(i + 1) * W]), rtol=1e-12)
+
+
+def test_history_is_consistent_with_walk_results(gpu_available):
+    """The recorder's own invariants on a larger solve: path[0] is the query point,
+    each walk's value is the float32 sum of its contributions in order, and the
+    recorded walks are the same walks solve_walks() returns."""
+    sc, s = _solver_for("dcr_dipole")
+    pts = sc.points[18:22]
+    W = 256
+    u, hist = s.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=8, return_history=True)
+    v, st = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=8)
+    for i in range(len(pts)):
+        for j, w in enumerate(hist[i]):
+            assert w["steps"] == st[i, j] and np.float32(w["value"]) == v[i, j]
+            if w["steps"]:
+                np.testing.assert_array_equal(np.asarray(w["path"][0]["point"], np.float32), pts[i])
+            acc = np.float32(0.0)
+            for c in w["contributions"]:
+                acc = np.float32(acc + np.float32(c["contribution"]))
+            assert acc == v[i, j]
+
+
 def _diag(got, ref):
     d = np.abs(np.asarray(got, np.float64) - np.asarray(ref, np.float64))
     rel = d / np.maximum(np.abs(ref), 1e-30)
@@ -167,10 +254,9 @@ def test_device_matches_oracle(gpu_available, name):
     npts, W = SENS_SIZES[name]
     pts = sensitivity_points(sc, name, npts)
     seed = 31337
-    u, hist, st = s.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=seed, return_history=True,
-                          return_stats=True)
-    gv = np.array([w["value"] for i in range(npts) for w in hist[i]], np.float32)
-    gs = np.array([w["steps"] for i in range(npts) for w in hist[i]])
+    u, st = s.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=seed, return_stats=True)
+    gv, gs = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=seed)
+    gv, gs = gv.ravel(), gs.ravel()
     pb = O.Problem.from_scenario(sc, sigma_bar=s.sigma_bar or 0.0)
     ov, os_ = pb.solve_walks(pts, W, sc.max_steps, sc.eps, seed)
     scale = max(np.abs(ov).max(), 1e-30)
@@ -197,10 +283,8 @@ def test_statistics_vs_reference_rng(gpu_available, name):
     sc, s = _solver_for(name)
     W = STAT_WALKS[name]
     npts = len(z["points"])
-    u, hist = s.solve(z["points"], nWalks=W, maxSteps=int(z["max_steps"]), eps=float(z["eps"]), seed=77,
-                      return_history=True)
-    v = np.array([[w["value"] for w in hist[i]] for i in range(npts)], np.float64)
-    st = np.array([[w["steps"] for w in hist[i]] for i in range(npts)], np.float64)
+    v, st = s.solve_walks(z["points"], nWalks=W, maxSteps=int(z["max_steps"]), eps=float(z["eps"]), seed=77)
+    v, st = v.astype(np.float64), st.astype(np.float64)
     p = bootstrap_pvalues(v, int(z["n_walks"]), z["mean"])
     assert p.min() > 1e-3, p
     ps = bootstrap_pvalues(st, int(z["n_walks"]), z["mean_steps"], seed=1)
@@ -242,15 +326,11 @@ def test_jit_kernel_matches_interpreted_kernel(gpu_available, name):
     sc, s = _solver_for(name)
     pts = sc.points[:8]
     W = 2048
-    u1, h1 = s.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=3, return_history=True)
+    v1, s1 = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=3)
     assert s.last_timing["jit"] == 1, "the field-specialised kernel did not build"
     s.set_jit(False)
-    u0, h0 = s.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=3, return_history=True)
+    v0, s0 = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=3)
     assert s.last_timing["jit"] == 0
-    v1 = np.array([w["value"] for i in range(len(pts)) for w in h1[i]], np.float32)
-    v0 = np.array([w["value"] for i in range(len(pts)) for w in h0[i]], np.float32)
-    s1 = np.array([w["steps"] for i in range(len(pts)) for w in h1[i]])
-    s0 = np.array([w["steps"] for i in range(len(pts)) for w in h0[i]])
     assert np.array_equal(s1, s0)
     assert np.array_equal(v1.view(np.uint32), v0.view(np.uint32)) or np.array_equal(v1, v0)
 

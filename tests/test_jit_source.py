@@ -18,12 +18,12 @@ HIPRTC_OPTS = ["-O3", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt", 
 def test_generated_sources_name_their_variant():
     src = S.dcr_dipole().kernel_source()
     assert "walk kernel, mode 5" in src and "wost_walk_jit" in src
-    assert "walk_body<true, true, true, false>" in src
+    assert "walk_body<true, true, true, false, false>" in src
     assert "const float2 v[5]" in src                       # the square compiled in
     topo = S.wenner_topography(n_electrodes=4, n_walks=1).kernel_source()
-    assert "walk_body<true, true, true, true>" in topo      # the 10k-segment surface uses the tree
+    assert "walk_body<true, true, true, true, false>" in topo      # the 10k-segment surface uses the tree
     lap = S.laplace_square().kernel_source()
-    assert "walk_body<false, false, false, false>" in lap
+    assert "walk_body<false, false, false, false, false>" in lap
 
 
 def test_generated_sources_compile_for_gfx950():

@@ -129,12 +129,9 @@ def test_gpu_tree_walks_match_scan_walks(gpu_available):
             s = sc.solver(device=0)
             s.set_segment_tree(0 if tree else -1)
             s.set_jit(jit)
-            u, hist = s.solve(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=9,
-                              return_history=True)
+            v, st = s.solve_walks(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=9)
             assert s.last_timing["tree"] == int(tree)
-            v = np.array([w["value"] for i in range(len(sc.points)) for w in hist[i]], np.float32)
-            st = np.array([w["steps"] for i in range(len(sc.points)) for w in hist[i]])
-            res[(tree, jit)] = (v, st)
+            res[(tree, jit)] = (v.ravel(), st.ravel())
     ref = res[(False, True)]
     for key, (v, st) in res.items():
         np.testing.assert_array_equal(st, ref[1], err_msg=str(key))

@@ -377,15 +377,31 @@ def replay(name, points, n_walks, max_steps, eps, seed):
         torch.rand = orig_rand
         ref_mod.GreensDistribution2D, ref_mod.ScreenedGreensDistribution2D = oG, oS
     vals, steps, finals = [], [], []
+    # the recorded histories themselves (golden vectors of the walk recorder)
+    path_pts, path_dd, path_dn, src_pts, src_vals, bnd_vals, totals = [], [], [], [], [], [], []
+    f32 = lambda v: float(v.item()) if isinstance(v, torch.Tensor) else (float("nan") if v is None else float(v))
     for pi in range(len(points)):
         for wk in hist[pi]:
             vals.append(sum(c["contribution"] for c in wk["contributions"]))
             steps.append(len(wk["path"]))
             finals.append(wk["contributions"][-1]["point"].detach().numpy())
+            for st in wk["path"]:
+                path_pts.append(st["point"].detach().numpy().astype(np.float32))
+                path_dd.append(f32(st["dirichlet_distance"]))
+                path_dn.append(f32(st["neumann_distance"]))
+            for c in wk["contributions"][:-1]:
+                src_pts.append(c["point"].detach().numpy().astype(np.float32))
+                src_vals.append(f32(c["contribution"]))
+            bnd_vals.append(f32(wk["contributions"][-1]["contribution"]))
+            totals.append(f32(wk["total_contribution"]))
     res = dict(points=points, n_walks=np.int64(n_walks), max_steps=np.int64(max_steps), eps=np.float32(eps),
                seed=np.uint64(seed), walk_values=np.array(vals, np.float64), walk_steps=np.array(steps, np.int64),
                final_points=np.array(finals, np.float32), u=u.detach().numpy().astype(np.float32).ravel(), nodes=nodes,
-               dirichlet=solver.dirichletBoundary.points.numpy().astype(np.float32))
+               dirichlet=solver.dirichletBoundary.points.numpy().astype(np.float32),
+               path_points=np.array(path_pts, np.float32).reshape(-1, 2), path_dd=np.array(path_dd, np.float32),
+               path_dn=np.array(path_dn, np.float32), src_points=np.array(src_pts, np.float32).reshape(-1, 2),
+               src_values=np.array(src_vals, np.float32), boundary_values=np.array(bnd_vals, np.float32),
+               total_contribution=np.array(totals, np.float64))
     if solver.neumannBoundary is not None:
         res["neumann"] = solver.neumannBoundary.points.numpy().astype(np.float32)
     if solver.use_delta_tracking:
