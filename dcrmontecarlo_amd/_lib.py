@@ -21,6 +21,7 @@ WOST_ERR_NO_DEVICE = -3
 WOST_ERR_UNSUPPORTED = -4
 WOST_ERR_OOM = -5
 
+ABI_VERSION = 2   # include/wost.h WOST_ABI_VERSION
 WOST_BLOCK_WALKS = 4096
 WOST_SAMPLER_TABLE_N = 4097
 COMPAT = {"reference": 0, "fixed": 1}
@@ -39,7 +40,8 @@ class WostTerm(ctypes.Structure):
 
 class WostField(ctypes.Structure):
     _fields_ = [("terms", POINTER(WostTerm)), ("n_terms", c_int32),
-                ("factors", POINTER(WostFactor)), ("n_factors", c_int32), ("flags", c_int32)]
+                ("factors", POINTER(WostFactor)), ("n_factors", c_int32), ("flags", c_int32),
+                ("grid", POINTER(c_float)), ("n_grid", c_int64)]
 
 
 class WostPolyline(ctypes.Structure):
@@ -98,8 +100,8 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.wost_version() != 1:
-        raise ImportError(f"libwost ABI version {lib.wost_version()} != 1")
+    if lib.wost_version() != ABI_VERSION:
+        raise ImportError(f"libwost ABI version {lib.wost_version()} != {ABI_VERSION} (rebuild libwost.so)")
     return lib
 
 
@@ -158,9 +160,10 @@ def make_field(field):
         F[i].kind = kind
         for k in range(8):
             F[i].p[k] = np.float32(p[k])
+    G = field.grid_values()
     wf = WostField(ctypes.cast(T, POINTER(WostTerm)), len(terms), ctypes.cast(F, POINTER(WostFactor)),
-                   len(factors), field.flags)
-    return wf, (T, F, wf)
+                   len(factors), field.flags, fptr(G) if G.size else None, int(G.size))
+    return wf, (T, F, G, wf)
 
 
 def declared_symbols() -> list[str]:

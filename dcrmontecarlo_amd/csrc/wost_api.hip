@@ -48,6 +48,7 @@ struct HostField {
     int flags = 0;
     std::vector<DTerm> terms;      // first = index into this field's factors
     std::vector<DFactor> factors;
+    std::vector<float> grid;       // FK_GRID values; p6 = offset into this field's grid
 };
 
 int convert_field(const wost_field* in, HostField& out, const char* name) {
@@ -58,12 +59,25 @@ int convert_field(const wost_field* in, HostField& out, const char* name) {
         return fail(WOST_ERR_INVALID_ARG, "field %s: bad term/factor arrays", name);
     if (in->n_terms > 4096 || in->n_factors > 16384)
         return fail(WOST_ERR_INVALID_ARG, "field %s: too many terms/factors", name);
+    if (in->n_grid < 0 || in->n_grid > WOST_MAX_GRID_VALUES || (in->n_grid > 0 && !in->grid))
+        return fail(WOST_ERR_INVALID_ARG, "field %s: bad grid array (%lld values)", name, (long long)in->n_grid);
     out.present = true;
     out.flags = in->flags;
     for (int i = 0; i < in->n_factors; ++i) {
         const wost_factor& f = in->factors[i];
-        if (f.kind < WOST_FK_MONO || f.kind > WOST_FK_IND_DISK)
+        if (f.kind < WOST_FK_MONO || f.kind > WOST_FK_GRID)
             return fail(WOST_ERR_INVALID_ARG, "field %s: factor %d has unknown kind %d", name, i, f.kind);
+        if (f.kind == WOST_FK_GRID) {
+            const float nx = f.p[4], ny = f.p[5], off = f.p[6];
+            const bool ints = nx == std::floor(nx) && ny == std::floor(ny) && off == std::floor(off);
+            if (!ints || !(nx >= 2.f && ny >= 2.f && off >= 0.f) ||
+                (double)off + (double)nx * (double)ny > (double)in->n_grid)
+                return fail(WOST_ERR_INVALID_ARG, "field %s: grid factor %d (%g x %g at %g) exceeds the %lld grid values",
+                            name, i, nx, ny, off, (long long)in->n_grid);
+            if (!(std::isfinite(f.p[0]) && std::isfinite(f.p[1]) && f.p[2] > 0.f && f.p[3] > 0.f &&
+                  std::isfinite(f.p[2]) && std::isfinite(f.p[3])))
+                return fail(WOST_ERR_INVALID_ARG, "field %s: grid factor %d has a bad origin or spacing", name, i);
+        }
         if (f.kind == WOST_FK_MONO) {
             for (int q = 0; q < 2; ++q) {
                 float e = f.p[q];
@@ -86,6 +100,7 @@ int convert_field(const wost_field* in, HostField& out, const char* name) {
         d.nf = tm.n_factors;
         out.terms.push_back(d);
     }
+    if (in->n_grid > 0) out.grid.assign(in->grid, in->grid + in->n_grid);
     return WOST_OK;
 }
 
@@ -98,36 +113,50 @@ struct Program {
         return reinterpret_cast<const DFactor*>(bytes.data() + sizeof(DProgram) +
                                                 sizeof(DTerm) * hdr()->n_terms_total);
     }
+    const float* grid() const {
+        return reinterpret_cast<const float*>(bytes.data() +
+                                              program_grid_offset(hdr()->n_terms_total, hdr()->n_factors_total));
+    }
 };
 
 void build_program(const HostField* f, double sigma_bar, Program& out) {
     DProgram hdr{};
     std::vector<DTerm> terms;
     std::vector<DFactor> factors;
+    std::vector<float> grid;
     for (int s = 0; s < N_SLOTS; ++s) {
         hdr.field[s].present = f[s].present ? 1 : 0;
         hdr.field[s].flags = f[s].flags;
         hdr.field[s].first_term = (int)terms.size();
         hdr.field[s].n_terms = (int)f[s].terms.size();
         const int fbase = (int)factors.size();
+        const float gbase = (float)grid.size();   // exact: < 2^24 per field, checked on input
         for (DTerm t : f[s].terms) {
             t.first += fbase;
             terms.push_back(t);
         }
-        for (const DFactor& d : f[s].factors) factors.push_back(d);
+        for (DFactor d : f[s].factors) {
+            if (d.kind == WOST_FK_GRID) d.p[6] += gbase;
+            factors.push_back(d);
+        }
+        grid.insert(grid.end(), f[s].grid.begin(), f[s].grid.end());
     }
     fit_i0e_chebyshev(hdr.cheb_a, kChebA, hdr.cheb_b, kChebB);
     hdr.sigma_bar = (float)sigma_bar;
     hdr.sqrt_sigma_bar = (float)std::sqrt(sigma_bar > 0 ? sigma_bar : 0.0);
     hdr.inv_sigma_bar = sigma_bar > 0 ? (float)(1.0 / sigma_bar) : 0.f;
     hdr.n_terms_total = (int)terms.size();
-    out.bytes.assign(sizeof(DProgram) + sizeof(DTerm) * terms.size() + sizeof(DFactor) * factors.size(), 0);
+    hdr.n_factors_total = (int)factors.size();
+    hdr.n_grid_total = (int)grid.size();
+    const size_t goff = program_grid_offset(hdr.n_terms_total, hdr.n_factors_total);
+    out.bytes.assign(goff + sizeof(float) * grid.size(), 0);
     std::memcpy(out.bytes.data(), &hdr, sizeof(hdr));
     if (!terms.empty())
         std::memcpy(out.bytes.data() + sizeof(DProgram), terms.data(), sizeof(DTerm) * terms.size());
     if (!factors.empty())
         std::memcpy(out.bytes.data() + sizeof(DProgram) + sizeof(DTerm) * terms.size(), factors.data(),
                     sizeof(DFactor) * factors.size());
+    if (!grid.empty()) std::memcpy(out.bytes.data() + goff, grid.data(), sizeof(float) * grid.size());
 }
 
 // torch.linspace(start, end, steps) in float32 (ATen CPU kernel: the first half
@@ -274,8 +303,8 @@ double estimate_sigma_bar(const wost_handle* h, const Program& prog) {
     float lo = INFINITY, hi = -INFINITY;
     for (float x : gx) {
         for (float y : gy) {
-            Jet aj = field_jet(fa, prog.terms(), prog.factors(), x, y);
-            float sg = fs.present ? field_value(fs, prog.terms(), prog.factors(), x, y) : 0.f;
+            Jet aj = field_jet(fa, prog.terms(), prog.factors(), prog.grid(), x, y);
+            float sg = fs.present ? field_value(fs, prog.terms(), prog.factors(), prog.grid(), x, y) : 0.f;
             float sp = sigma_prime_from(aj, sg, detached);
             if (std::isnan(sp) || std::isinf(sp)) continue;
             any = true;

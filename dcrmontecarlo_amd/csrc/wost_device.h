@@ -124,8 +124,16 @@ struct alignas(16) DProgram {
     float sqrt_sigma_bar;
     float inv_sigma_bar;
     int32_t n_terms_total;
-    // DTerm terms[n_terms_total] follows at offset sizeof(DProgram), then DFactor[]
+    int32_t n_factors_total;
+    int32_t n_grid_total;
+    // DTerm terms[n_terms_total] follows at offset sizeof(DProgram), then
+    // DFactor factors[n_factors_total], then float grid[n_grid_total]
 };
+
+// Byte offset of the tabulated grid values in a program buffer.
+WOST_HD size_t program_grid_offset(int n_terms, int n_factors) {
+    return sizeof(DProgram) + sizeof(DTerm) * (size_t)n_terms + sizeof(DFactor) * (size_t)n_factors;
+}
 
 struct Jet { float v, gx, gy, lap; };
 
@@ -224,8 +232,79 @@ WOST_HD Jet fj_ind_box(float x, float y, float x0, float x1, float y0, float y1)
 }
 WOST_HD Jet fj_ind_disk(float x, float y, float cx, float cy, float r2) { return jet_const(fv_ind_disk(x, y, cx, cy, r2)); }
 
+// ---- tabulated grid (WOST_FK_GRID): Catmull-Rom bicubic --------------------
+// The fallback for a coefficient callable that is not expressible with the
+// kinds above: the host tabulates it and the walk
+// interpolates. Per axis the position u = (x - x0)/h is clamped to the grid
+// [0, n-1] (constant extension, zero derivative outside); node i = floor(u)
+// and t = u - i weight nodes i-1..i+2 (indices clamped to the grid) with the
+// Keys a = -1/2 kernel, whose derivatives give the gradient and Laplacian.
+struct GridAxis {
+    int i0, i1, i2, i3;      // node indices
+    float w[4], d[4], s[4];  // weights and their first / second x-derivatives
+};
+
+WOST_HD GridAxis grid_axis(float x, float x0, float ih, int n) {
+    GridAxis a;
+    const float nm1 = (float)(n - 1);
+    float u = (x - x0) * ih;
+    const bool inside = u >= 0.0f && u <= nm1;
+    if (!(u == u)) u = 0.0f;                                  // NaN position: node 0
+    u = u < 0.0f ? 0.0f : (u > nm1 ? nm1 : u);
+    int i = (int)u;
+    if (i > n - 2) i = n - 2;
+    if (i < 0) i = 0;
+    const float t = u - (float)i, t2 = t * t, t3 = t2 * t;
+    a.i1 = i;
+    a.i0 = i > 0 ? i - 1 : 0;
+    a.i2 = i + 1 < n ? i + 1 : n - 1;
+    a.i3 = i + 2 < n ? i + 2 : n - 1;
+    a.w[0] = 0.5f * (-t3 + 2.0f * t2 - t);
+    a.w[1] = 0.5f * (3.0f * t3 - 5.0f * t2 + 2.0f);
+    a.w[2] = 0.5f * (-3.0f * t3 + 4.0f * t2 + t);
+    a.w[3] = 0.5f * (t3 - t2);
+    const float g1 = inside ? ih : 0.0f, g2 = g1 * g1;
+    a.d[0] = g1 * (0.5f * (-3.0f * t2 + 4.0f * t - 1.0f));
+    a.d[1] = g1 * (0.5f * (9.0f * t2 - 10.0f * t));
+    a.d[2] = g1 * (0.5f * (-9.0f * t2 + 8.0f * t + 1.0f));
+    a.d[3] = g1 * (0.5f * (3.0f * t2 - 2.0f * t));
+    a.s[0] = g2 * (-3.0f * t + 2.0f);
+    a.s[1] = g2 * (9.0f * t - 5.0f);
+    a.s[2] = g2 * (-9.0f * t + 4.0f);
+    a.s[3] = g2 * (3.0f * t - 1.0f);
+    return a;
+}
+
+WOST_HD float grid_row(const float* row, const GridAxis& ax, const float* w) {
+    return w[0] * row[ax.i0] + w[1] * row[ax.i1] + w[2] * row[ax.i2] + w[3] * row[ax.i3];
+}
+
+WOST_HD float fv_grid(const float* g, float x, float y, float x0, float y0, float ihx, float ihy, int nx, int ny) {
+    const GridAxis ax = grid_axis(x, x0, ihx, nx), ay = grid_axis(y, y0, ihy, ny);
+    const int rows[4] = {ay.i0, ay.i1, ay.i2, ay.i3};
+    float v = 0.0f;
+    for (int j = 0; j < 4; ++j) v = v + ay.w[j] * grid_row(g + (size_t)rows[j] * (size_t)nx, ax, ax.w);
+    return v;
+}
+
+WOST_HD Jet fj_grid(const float* g, float x, float y, float x0, float y0, float ihx, float ihy, int nx, int ny) {
+    const GridAxis ax = grid_axis(x, x0, ihx, nx), ay = grid_axis(y, y0, ihy, ny);
+    const int rows[4] = {ay.i0, ay.i1, ay.i2, ay.i3};
+    Jet r{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) {
+        const float* row = g + (size_t)rows[j] * (size_t)nx;
+        const float rv = grid_row(row, ax, ax.w), rd = grid_row(row, ax, ax.d), rs = grid_row(row, ax, ax.s);
+        r.v = r.v + ay.w[j] * rv;
+        r.gx = r.gx + ay.w[j] * rd;
+        r.gy = r.gy + ay.d[j] * rv;
+        r.lap = r.lap + (ay.w[j] * rs + ay.s[j] * rv);
+    }
+    return r;
+}
+
 // ---- dispatch over a program factor (interpreter) ---------------------------
-WOST_HD float factor_value(const DFactor& f, float x, float y) {
+// grid: base of the program's tabulated values (FK_GRID p6 indexes into it).
+WOST_HD float factor_value(const DFactor& f, float x, float y, const float* grid) {
     const float* p = f.p;
     switch (f.kind) {
     case WOST_FK_MONO: return fv_mono(x, y, (int)p[0], (int)p[1]);
@@ -236,11 +315,12 @@ WOST_HD float factor_value(const DFactor& f, float x, float y) {
     case WOST_FK_SIGMOID_RADIAL: return fv_sigmoid_radial(x, y, p[0], p[1], p[2], p[3]);
     case WOST_FK_IND_BOX: return fv_ind_box(x, y, p[0], p[1], p[2], p[3]);
     case WOST_FK_IND_DISK: return fv_ind_disk(x, y, p[0], p[1], p[2]);
+    case WOST_FK_GRID: return fv_grid(grid + (int)p[6], x, y, p[0], p[1], p[2], p[3], (int)p[4], (int)p[5]);
     default: return WOST_NAN;
     }
 }
 
-WOST_HD Jet factor_jet(const DFactor& f, float x, float y) {
+WOST_HD Jet factor_jet(const DFactor& f, float x, float y, const float* grid) {
     const float* p = f.p;
     switch (f.kind) {
     case WOST_FK_MONO: return fj_mono(x, y, (int)p[0], (int)p[1]);
@@ -251,22 +331,24 @@ WOST_HD Jet factor_jet(const DFactor& f, float x, float y) {
     case WOST_FK_SIGMOID_RADIAL: return fj_sigmoid_radial(x, y, p[0], p[1], p[2], p[3]);
     case WOST_FK_IND_BOX: return fj_ind_box(x, y, p[0], p[1], p[2], p[3]);
     case WOST_FK_IND_DISK: return fj_ind_disk(x, y, p[0], p[1], p[2]);
+    case WOST_FK_GRID: return fj_grid(grid + (int)p[6], x, y, p[0], p[1], p[2], p[3], (int)p[4], (int)p[5]);
     default: return Jet{WOST_NAN, 0.f, 0.f, 0.f};
     }
 }
 
 // Field evaluation. TP/FP are pointer types to DTerm/DFactor: plain pointers
 // on the host, constant-address-space views on the device so that the
-// wave-uniform reads become scalar (SMEM) loads.
+// wave-uniform reads become scalar (SMEM) loads. grid: the program's
+// tabulated values (global memory: the gathers are per lane).
 template <class TP, class FP>
-WOST_HD float field_value(const DField& fd, TP terms, FP factors, float x, float y) {
+WOST_HD float field_value(const DField& fd, TP terms, FP factors, const float* grid, float x, float y) {
     float acc = 0.0f;
     for (int t = 0; t < fd.n_terms; ++t) {
         DTerm tm = terms[fd.first_term + t];
         float prod = tm.coef;
         for (int k = 0; k < tm.nf; ++k) {
             DFactor f = factors[tm.first + k];
-            prod = prod * factor_value(f, x, y);
+            prod = prod * factor_value(f, x, y, grid);
         }
         acc = acc + prod;
     }
@@ -276,7 +358,7 @@ WOST_HD float field_value(const DField& fd, TP terms, FP factors, float x, float
 // Term jets: constant term -> jet_const(c); otherwise jet_scale(c, first
 // factor) then jet_mul with the others.
 template <class TP, class FP>
-WOST_HD Jet field_jet(const DField& fd, TP terms, FP factors, float x, float y) {
+WOST_HD Jet field_jet(const DField& fd, TP terms, FP factors, const float* grid, float x, float y) {
     Jet acc = jet_const(0.0f);
     for (int t = 0; t < fd.n_terms; ++t) {
         DTerm tm = terms[fd.first_term + t];
@@ -284,8 +366,8 @@ WOST_HD Jet field_jet(const DField& fd, TP terms, FP factors, float x, float y) 
         if (tm.nf == 0) {
             prod = jet_const(tm.coef);
         } else {
-            prod = jet_scale(tm.coef, factor_jet(factors[tm.first], x, y));
-            for (int k = 1; k < tm.nf; ++k) prod = jet_mul(prod, factor_jet(factors[tm.first + k], x, y));
+            prod = jet_scale(tm.coef, factor_jet(factors[tm.first], x, y, grid));
+            for (int k = 1; k < tm.nf; ++k) prod = jet_mul(prod, factor_jet(factors[tm.first + k], x, y, grid));
         }
         acc = jet_add(acc, prod);
     }

@@ -67,6 +67,10 @@ std::string factor_call(const DFactor& f, bool jet) {
     case WOST_FK_IND_DISK:
         o << pre << "ind_disk(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ")";
         break;
+    case WOST_FK_GRID:   // values stay in the program buffer (grid = its tabulated part)
+        o << pre << "grid(grid + " << (int)p[6] << ", x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2])
+          << ", " << lit(p[3]) << ", " << (int)p[4] << ", " << (int)p[5] << ")";
+        break;
     default:
         o << (jet ? "wost::Jet{__builtin_nanf(\"\"), 0.f, 0.f, 0.f}" : "__builtin_nanf(\"\")");
     }
@@ -199,7 +203,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     const DField& fA = hdr.field[SLOT_ALPHA];
     std::ostringstream o;
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
-      << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n";
+      << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
+      << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
     o << "    __device__ __forceinline__ bool has_g() const { return " << (fG.present ? "true" : "false") << "; }\n";
     o << "    __device__ __forceinline__ float g(float x, float y) const {\n"
       << (fG.present ? value_body(fG, terms, factors) : "        return 0.0f;\n") << "    }\n";
@@ -254,7 +259,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "extern \"C\" __global__ void __launch_bounds__(wost::kWalkBlock, " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
-      << "    const GenFields fld;\n"
+      << "    const GenFields fld{reinterpret_cast<const float*>(A.prog + "
+      << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
       << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
       << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
       << ">(A, fld, smem);\n}\n";

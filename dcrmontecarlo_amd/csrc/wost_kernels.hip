@@ -54,10 +54,12 @@ struct ProgView {
     cptr<DProgram> hdr;
     TermsC terms;
     FactorsC factors;
+    const float* grid;   // tabulated values: per-lane gathers, so a plain global pointer
     __device__ __forceinline__ explicit ProgView(const char* prog) {
         hdr = (cptr<DProgram>)prog;
         terms.p = (cptr<DTerm>)(prog + sizeof(DProgram));
         factors.p = (cptr<DFactor>)(prog + sizeof(DProgram) + sizeof(DTerm) * hdr->n_terms_total);
+        grid = reinterpret_cast<const float*>(prog + program_grid_offset(hdr->n_terms_total, hdr->n_factors_total));
     }
     __device__ __forceinline__ DField field(int slot) const {
         DField f;
@@ -68,10 +70,10 @@ struct ProgView {
         return f;
     }
     __device__ __forceinline__ float value(const DField& f, float x, float y) const {
-        return field_value(f, terms, factors, x, y);
+        return field_value(f, terms, factors, grid, x, y);
     }
     __device__ __forceinline__ Jet jet(const DField& f, float x, float y) const {
-        return field_jet(f, terms, factors, x, y);
+        return field_jet(f, terms, factors, grid, x, y);
     }
 };
 

@@ -38,7 +38,7 @@ __all__ = [
     "Field", "X", "Y", "const", "as_field", "exp", "sin", "cos", "sigmoid",
     "sigmoid_radial", "smooth_circle", "gaussian", "indicator_box", "indicator_disk",
     "detach", "FK_MONO", "FK_EXP_QUAD", "FK_SIN_LIN", "FK_COS_LIN", "FK_SIGMOID_LIN",
-    "FK_SIGMOID_RADIAL", "FK_IND_BOX", "FK_IND_DISK", "FIELD_DETACHED",
+    "FK_SIGMOID_RADIAL", "FK_IND_BOX", "FK_IND_DISK", "FK_GRID", "FIELD_DETACHED", "tabulated",
 ]
 
 # include/wost.h enum wost_factor_kind
@@ -50,17 +50,25 @@ FK_SIGMOID_LIN = 5
 FK_SIGMOID_RADIAL = 6
 FK_IND_BOX = 7
 FK_IND_DISK = 8
+FK_GRID = 9
 FIELD_DETACHED = 1
 
 _MAX_EXP = 15
+_MAX_GRID_VALUES = 1 << 22     # include/wost.h WOST_MAX_GRID_VALUES
+_grid_ids = iter(range(1, 1 << 62))
 
 
 class _Factor(tuple):
-    """(kind, params[8]) -- params stored as Python floats (double) until packed."""
+    """(kind, params[8]) -- params stored as Python floats (double) until packed.
+    A FK_GRID factor also carries its values (``.data``, float32 [ny, nx]); its
+    p6 (offset) is assigned by :meth:`Field.pack` and p7 holds a unique id so
+    that different grids never merge."""
 
-    def __new__(cls, kind: int, params: Sequence[float]):
+    def __new__(cls, kind: int, params: Sequence[float], data=None):
         p = tuple(float(v) for v in params) + (0.0,) * (8 - len(params))
-        return super().__new__(cls, (int(kind), p))
+        self = super().__new__(cls, (int(kind), p))
+        self.data = data
+        return self
 
     @property
     def kind(self) -> int:
@@ -172,16 +180,47 @@ class Field:
 
     # ---- packing (include/wost.h wost_field) --------------------------------
     def pack(self):
-        """(terms, factors): terms = [(coef, first, n)], factors = [(kind, p[8])] as float32-ready."""
+        """(terms, factors): terms = [(coef, first, n)], factors = [(kind, p[8])] as float32-ready.
+        A grid factor's p6 is the offset of its values in :meth:`grid_values`."""
         terms, factors = [], []
+        offsets = self._grid_offsets()
         for t in self.terms:
             first = len(factors)
             if t.mono != (0, 0):
                 factors.append((FK_MONO, (float(t.mono[0]), float(t.mono[1])) + (0.0,) * 6))
             for f in t.factors:
-                factors.append((f.kind, f.params))
+                p = f.params
+                if f.kind == FK_GRID:
+                    p = p[:6] + (float(offsets[id(f.data)]), 0.0)
+                factors.append((f.kind, p))
             terms.append((t.coef, first, len(factors) - first))
         return terms, factors
+
+    def _grids(self):
+        seen, out = set(), []
+        for t in self.terms:
+            for f in t.factors:
+                if f.kind == FK_GRID and id(f.data) not in seen:
+                    seen.add(id(f.data))
+                    out.append(f.data)
+        return out
+
+    def _grid_offsets(self) -> dict:
+        off, pos = {}, 0
+        for g in self._grids():
+            off[id(g)] = pos
+            pos += g.size
+        return off
+
+    def grid_values(self) -> np.ndarray:
+        """All grid factors' values, concatenated (float32, row-major [ny, nx] each)."""
+        gs = self._grids()
+        if not gs:
+            return np.zeros(0, np.float32)
+        return np.ascontiguousarray(np.concatenate([g.ravel() for g in gs]), dtype=np.float32)
+
+    def is_tabulated(self) -> bool:
+        return bool(self._grids())
 
     # ---- host evaluation (reference calling convention) --------------------
     def __call__(self, point):
@@ -299,6 +338,24 @@ def indicator_disk(center, radius: float) -> Field:
     return Field([_Term(1.0, (0, 0), [_Factor(FK_IND_DISK, (center[0], center[1], float(radius) ** 2))])])
 
 
+def tabulated(values, x0: float, y0: float, hx: float, hy: float) -> Field:
+    """A field interpolated from values on a regular grid (include/wost.h
+    WOST_FK_GRID): node (i, j) at (x0 + i*hx, y0 + j*hy) holds values[j, i].
+    Catmull-Rom bicubic between nodes, constant outside the grid. This is what
+    an arbitrary Python callable becomes when it cannot be traced into the
+    closed-form factors (dcrmontecarlo_amd.trace)."""
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    if v.ndim != 2 or v.shape[0] < 2 or v.shape[1] < 2:
+        raise ValueError(f"tabulated() needs a [ny, nx] array with nx, ny >= 2, got shape {v.shape}")
+    if v.size > _MAX_GRID_VALUES:
+        raise ValueError(f"tabulated(): {v.size} values exceed the limit of {_MAX_GRID_VALUES}")
+    if not (hx > 0 and hy > 0):
+        raise ValueError("tabulated(): grid spacings must be positive")
+    ny, nx = v.shape
+    p = (x0, y0, 1.0 / float(hx), 1.0 / float(hy), float(nx), float(ny), 0.0, float(next(_grid_ids)))
+    return Field([_Term(1.0, (0, 0), [_Factor(FK_GRID, p, data=v)])])
+
+
 def detach(f) -> Field:
     """Mark alpha as not differentiable by the reference's autograd.
 
@@ -357,7 +414,67 @@ def _factor_numpy(fc: _Factor, x, y):
     if k == FK_IND_DISK:
         dx, dy = x - p[0], y - p[1]
         return (dx * dx + dy * dy <= p[2]).astype(np.float32)
+    if k == FK_GRID:
+        return _grid_numpy(fc, x, y)
     raise ValueError(f"unknown factor kind {k}")
+
+
+def _cr_weights(t):
+    """Catmull-Rom (Keys a = -1/2) weights of nodes i-1..i+2 at t in [0, 1]."""
+    t2 = t * t
+    t3 = t2 * t
+    h = 0.5   # a weak Python scalar: float32 stays float32 (numpy >= 2, torch)
+    return (h * (-t3 + 2 * t2 - t), h * (3 * t3 - 5 * t2 + 2), h * (-3 * t3 + 4 * t2 + t), h * (t3 - t2))
+
+
+def _grid_axis_numpy(x, x0, ih, n):
+    f32 = np.float32
+    u = (x - f32(x0)) * f32(ih)
+    u = np.where(np.isnan(u), f32(0), u)
+    u = np.clip(u, f32(0), f32(n - 1)).astype(np.float32)
+    i = np.clip(np.floor(u).astype(np.int64), 0, n - 2)
+    t = (u - i.astype(np.float32)).astype(np.float32)
+    idx = [np.clip(i + o, 0, n - 1) for o in (-1, 0, 1, 2)]
+    return idx, _cr_weights(t)
+
+
+def _grid_numpy(fc: _Factor, x, y):
+    p = fc.params
+    data = fc.data
+    ny, nx = data.shape
+    ix, wx = _grid_axis_numpy(np.asarray(x, np.float32), p[0], np.float32(p[2]), nx)
+    iy, wy = _grid_axis_numpy(np.asarray(y, np.float32), p[1], np.float32(p[3]), ny)
+    acc = np.zeros(np.shape(x), np.float32)
+    for j in range(4):
+        row = np.zeros(np.shape(x), np.float32)
+        for i in range(4):
+            row = row + wx[i] * data[iy[j], ix[i]]
+        acc = acc + wy[j] * row
+    return acc
+
+
+def _grid_torch(fc: _Factor, x, y):
+    import torch
+
+    p = [float(np.float32(v)) for v in fc.params]
+    data = torch.from_numpy(fc.data).to(x.dtype)
+    ny, nx = fc.data.shape
+
+    def axis(v, x0, ih, n):
+        u = torch.nan_to_num((v - x0) * ih, nan=0.0).clamp(0.0, float(n - 1))
+        i = torch.floor(u.detach()).long().clamp(0, n - 2)
+        t = u - i.to(u.dtype)
+        return [(i + o).clamp(0, n - 1) for o in (-1, 0, 1, 2)], _cr_weights(t)
+
+    ix, wx = axis(x, p[0], p[2], nx)
+    iy, wy = axis(y, p[1], p[3], ny)
+    acc = torch.zeros_like(x)
+    for j in range(4):
+        row = torch.zeros_like(x)
+        for i in range(4):
+            row = row + wx[i] * data[iy[j], ix[i]]
+        acc = acc + wy[j] * row
+    return acc
 
 
 def _eval_torch(field: Field, point):
@@ -387,6 +504,8 @@ def _eval_torch(field: Field, point):
                 v = ((x >= p[0]) & (x <= p[1]) & (y >= p[2]) & (y <= p[3])).to(x.dtype)
             elif k == FK_IND_DISK:
                 v = (((x - p[0]) ** 2 + (y - p[1]) ** 2) <= p[2]).to(x.dtype)
+            elif k == FK_GRID:
+                v = _grid_torch(fc, x, y)
             else:
                 raise ValueError(f"unknown factor kind {k}")
             prod = prod * v

@@ -22,8 +22,11 @@ Field costs: per term 3, per factor value / jet as in _FACTOR_VALUE / _FACTOR_JE
 from __future__ import annotations
 
 # per-factor costs (value, jet incl. the product-rule multiply)
-_FACTOR_VALUE = {1: None, 2: 16, 3: 5, 4: 5, 5: 8, 6: 12, 7: 4, 8: 5}
-_FACTOR_JET = {1: None, 2: 50, 3: 32, 4: 32, 5: 36, 6: 50, 7: 24, 8: 25}
+_FACTOR_VALUE = {1: None, 2: 16, 3: 5, 4: 5, 5: 8, 6: 12, 7: 4, 8: 5, 9: 58}
+_FACTOR_JET = {1: None, 2: 50, 3: 32, 4: 32, 5: 36, 6: 50, 7: 24, 8: 25, 9: 160}
+# 9 (tabulated): per axis 16 for the Catmull-Rom weights (+18 derivatives, +12
+# second derivatives for the jet); 4 rows x 4 taps multiply-add = 32 (x3 for the
+# jet) plus the 4-row combination
 
 FP32_PEAK_TFLOPS = 157.3      # MI355X vector (= dense MFMA) FP32, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec

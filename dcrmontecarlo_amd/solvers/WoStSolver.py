@@ -8,8 +8,11 @@ kernel; this class only describes the problem and moves arrays.
 
 Differences a caller sees:
 
-* Coefficient functions must be device-evaluable fields
-  (:mod:`dcrmontecarlo_amd.fields`) or numbers, not arbitrary Python callables.
+* Coefficient functions become device-evaluable fields
+  (:mod:`dcrmontecarlo_amd.fields`): pass fields or numbers directly, or the
+  reference's Python callables, which are traced into closed form (exact) or
+  tabulated over the domain (approximate, with a warning) by
+  :mod:`dcrmontecarlo_amd.trace`.
 * Randomness is counter-based: ``solve(..., seed=0)`` is bitwise reproducible
   and independent of the GPU count. Walk ``i`` of point ``p`` uses Philox
   subsequence ``p*nWalks + i``.
@@ -51,6 +54,12 @@ def _field_or_none(f, what: str):
         return as_field(f)
     except TypeError as e:
         raise TypeError(f"{what}: {e}") from None
+
+
+def _bounds_of(dxy: np.ndarray, nxy) -> list:
+    allp = dxy if nxy is None else np.concatenate([dxy, nxy])
+    return [[float(allp[:, 0].min()), float(allp[:, 0].max())],
+            [float(allp[:, 1].min()), float(allp[:, 1].max())]]
 
 
 @dataclass
@@ -97,10 +106,11 @@ def kernel_source(dirichletBoundary, dirichletBoundaryFunction=None, neumannBoun
     arguments would compile (no device needed; wost_kernel_source)."""
     dxy = np.asarray(_np(dirichletBoundary.points), dtype=np.float32).reshape(-1, 2)
     nxy = None if neumannBoundary is None else np.asarray(_np(neumannBoundary.points), dtype=np.float32).reshape(-1, 2)
-    g = _field_or_none(dirichletBoundaryFunction, "dirichletBoundaryFunction")
-    f = _field_or_none(source, "source")
-    s = _field_or_none(sigma, "sigma")
-    a = _field_or_none(alpha, "alpha")
+    conv = _Converter(_bounds_of(dxy, nxy))
+    g = conv(dirichletBoundaryFunction, "dirichletBoundaryFunction")
+    f = conv(source, "source")
+    s = conv(sigma, "sigma")
+    a = conv(alpha, "alpha", is_alpha=True)
     if a is not None and a.is_constant():
         a = detach(a)
     prob, keep = _problem(dxy, nxy, g, f, s, a, "reference", 0, sigma_bar)
@@ -111,28 +121,55 @@ def kernel_source(dirichletBoundary, dirichletBoundaryFunction=None, neumannBoun
     return buf.value.decode()
 
 
+class _Converter:
+    """Coefficient arguments -> device fields: Fields and numbers as they are,
+    Python callables traced into closed form or tabulated over the domain
+    (dcrmontecarlo_amd.trace). Records how each one was converted."""
+
+    def __init__(self, bounds, resolution: int = 513, trace: bool = True):
+        self.bounds, self.resolution, self.trace = bounds, resolution, trace
+        self.log = {}
+
+    def __call__(self, obj, what: str, is_alpha: bool = False):
+        if obj is None:
+            return None
+        from ..trace import field_from_callable
+
+        c = field_from_callable(obj, self.bounds, what=what, is_alpha=is_alpha, resolution=self.resolution,
+                                trace_first=self.trace)
+        self.log[what] = c
+        return c.field
+
+
 class WostSolver_2D:
     """Walk-on-Stars solver for -div(alpha grad u) + sigma u = f with Dirichlet
-    and (optionally) Neumann polyline boundaries, on a HIP device."""
+    and (optionally) Neumann polyline boundaries, on a HIP device.
+
+    Coefficients (dirichletBoundaryFunction, source, sigma, alpha) may be
+    :mod:`dcrmontecarlo_amd.fields` fields, numbers, or the reference's Python
+    callables ``fn(point)``: those are traced into closed-form device fields,
+    or -- when they use something the tracer cannot express -- tabulated on a
+    ``grid_resolution``-node grid over the domain with a warning
+    (dcrmontecarlo_amd.trace). ``field_conversions`` records which."""
 
     def __init__(self, dirichletBoundary, dirichletBoundaryFunction=None, neumannBoundary=None,
                  source=None, sigma=None, alpha=None, *, compat: str = "reference", device: int | None = None,
-                 sigma_bar: float | None = None):
+                 sigma_bar: float | None = None, grid_resolution: int = 513, trace_callables: bool = True):
         self.dirichletBoundary = dirichletBoundary
         self.neumannBoundary = neumannBoundary
         dxy = np.asarray(_np(dirichletBoundary.points), dtype=np.float32).reshape(-1, 2)
         nxy = None if neumannBoundary is None else np.asarray(_np(neumannBoundary.points), dtype=np.float32).reshape(-1, 2)
-        allp = dxy if nxy is None else np.concatenate([dxy, nxy])
         # solvers/WoStSolver.py:37-43
-        self.domain_bounds = [[float(allp[:, 0].min()), float(allp[:, 0].max())],
-                              [float(allp[:, 1].min()), float(allp[:, 1].max())]]
-        self.boundaryDirichlet = _field_or_none(dirichletBoundaryFunction, "dirichletBoundaryFunction")
-        self.source = _field_or_none(source, "source")
+        self.domain_bounds = _bounds_of(dxy, nxy)
+        self._conv = _Converter(self.domain_bounds, grid_resolution, trace_callables)
+        self.field_conversions = self._conv.log
+        self.boundaryDirichlet = self._conv(dirichletBoundaryFunction, "dirichletBoundaryFunction")
+        self.source = self._conv(source, "source")
         self.use_delta_tracking = sigma is not None or alpha is not None     # :51-64
         self.sigma = self.alpha = None
         if self.use_delta_tracking:
-            s = _field_or_none(sigma, "sigma")
-            a = _field_or_none(alpha, "alpha")
+            s = self._conv(sigma, "sigma")
+            a = self._conv(alpha, "alpha", is_alpha=True)
             self.sigma = s if s is not None else const(0.0)                    # :55-56
             a = a if a is not None else const(1.0)                             # :57-58
             if a.is_constant():
@@ -165,13 +202,13 @@ class WostSolver_2D:
 
     # ---- setters (solvers/WoStSolver.py:141-157) ------------------------------
     def setBoundaryConditions(self, boundaryDirichlet):
-        self.boundaryDirichlet = _field_or_none(boundaryDirichlet, "boundaryDirichlet")
+        self.boundaryDirichlet = self._conv(boundaryDirichlet, "boundaryDirichlet")
         wf, keep = _lib.make_field(self.boundaryDirichlet)
         _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_BOUNDARY, ctypes.pointer(wf) if wf else None),
                    "setBoundaryConditions")
 
     def setSourceTerm(self, source):
-        self.source = _field_or_none(source, "source")
+        self.source = self._conv(source, "source")
         wf, keep = _lib.make_field(self.source)
         _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_SOURCE, ctypes.pointer(wf) if wf else None),
                    "setSourceTerm")

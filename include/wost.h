@@ -30,7 +30,7 @@ typedef unsigned long long uint64_t;
 extern "C" {
 #endif
 
-#define WOST_ABI_VERSION 1
+#define WOST_ABI_VERSION 2
 
 /* Walks of one query point are grouped in blocks of this many consecutive
  * walk indices. Per-block partial sums are the unit of reduction and of
@@ -81,8 +81,21 @@ enum wost_factor_kind {
     WOST_FK_SIGMOID_RADIAL = 6, /* 1/(1+exp(-p0 (sqrt((x-p1)^2+(y-p2)^2) - p3)))
                                    (utils.py:123-129 torch_smooth_circle is p0=-100) */
     WOST_FK_IND_BOX = 7,        /* 1 if p0<=x<=p1 and p2<=y<=p3 else 0 (zero gradient) */
-    WOST_FK_IND_DISK = 8        /* 1 if (x-p0)^2+(y-p1)^2 <= p2 else 0 (zero gradient) */
+    WOST_FK_IND_DISK = 8,       /* 1 if (x-p0)^2+(y-p1)^2 <= p2 else 0 (zero gradient) */
+    WOST_FK_GRID = 9            /* tabulated values (the fallback for a callable that is
+                                   not expressible with the kinds above):
+                                   Catmull-Rom bicubic interpolation of an nx x ny grid,
+                                   node (i,j) at (p0 + i/p2, p1 + j/p3), values
+                                   wost_field.grid[p6 + j*nx + i], nx = p4, ny = p5;
+                                   the position is clamped to the grid (constant
+                                   extension outside). C1, with an analytic gradient
+                                   and a piecewise Laplacian for sigma'. */
 };
+
+/* Largest grid a field may carry (floats, all its FK_GRID factors together;
+ * 2048 x 2048). Four fields together stay below 2^24, so offsets are exact
+ * in a float parameter. */
+#define WOST_MAX_GRID_VALUES (1 << 22)
 
 typedef struct {
     int32_t kind;   /* enum wost_factor_kind */
@@ -107,6 +120,8 @@ typedef struct {
     const wost_factor* factors;
     int32_t n_factors;
     int32_t flags;
+    const float* grid;      /* values of this field's WOST_FK_GRID factors (may be NULL) */
+    int64_t n_grid;         /* floats in grid, <= WOST_MAX_GRID_VALUES                 */
 } wost_field;
 
 /* A polyline: n_vertices points, xy = [x0,y0,x1,y1,...] float32

@@ -27,7 +27,7 @@ class OrcTerm(ctypes.Structure):
 
 class OrcField(ctypes.Structure):
     _fields_ = [("terms", POINTER(OrcTerm)), ("n_terms", c_int32), ("factors", POINTER(OrcFactor)),
-                ("n_factors", c_int32), ("flags", c_int32)]
+                ("n_factors", c_int32), ("flags", c_int32), ("grid", POINTER(c_float)), ("n_grid", c_int64)]
 
 
 class OrcProblem(ctypes.Structure):
@@ -93,9 +93,10 @@ def make_field(field):
         Fa[i].kind = k
         for j in range(8):
             Fa[i].p[j] = np.float32(p[j])
+    G = field.grid_values()
     of = OrcField(ctypes.cast(T, POINTER(OrcTerm)), len(terms), ctypes.cast(Fa, POINTER(OrcFactor)), len(factors),
-                  field.flags)
-    return of, (T, Fa, of)
+                  field.flags, _f(G) if G.size else None, int(G.size))
+    return of, (T, Fa, G, of)
 
 
 class Problem:

@@ -294,7 +294,60 @@ typedef struct { double v, gx, gy, l; } orc_jet;
 
 static double sigm(double z) { return 1.0 / (1.0 + exp(-z)); }
 
-static orc_jet orc_factor_jet(const orc_factor* f, double x, double y) {
+/* Catmull-Rom spline as a cubic Hermite segment between nodes 1 and 2 with
+ * tangents (P2-P0)/2 and (P3-P1)/2: weights of P0..P3 at t and their first
+ * and second t-derivatives. */
+static void orc_cr_basis(double t, double w[4], double d[4], double s[4]) {
+    double t2 = t * t, t3 = t2 * t;
+    double h00 = 2 * t3 - 3 * t2 + 1, h10 = t3 - 2 * t2 + t, h01 = -2 * t3 + 3 * t2, h11 = t3 - t2;
+    double d00 = 6 * t2 - 6 * t, d10 = 3 * t2 - 4 * t + 1, d01 = -6 * t2 + 6 * t, d11 = 3 * t2 - 2 * t;
+    double s00 = 12 * t - 6, s10 = 6 * t - 4, s01 = -12 * t + 6, s11 = 6 * t - 2;
+    w[0] = -0.5 * h10; w[1] = h00 - 0.5 * h11; w[2] = 0.5 * h10 + h01; w[3] = 0.5 * h11;
+    d[0] = -0.5 * d10; d[1] = d00 - 0.5 * d11; d[2] = 0.5 * d10 + d01; d[3] = 0.5 * d11;
+    s[0] = -0.5 * s10; s[1] = s00 - 0.5 * s11; s[2] = 0.5 * s10 + s01; s[3] = 0.5 * s11;
+}
+
+/* one axis of a tabulated factor: clamp to the grid (constant outside),
+ * node indices (clamped) and the derivative scale (0 outside) */
+static void orc_grid_axis(double x, double x0, double ih, int n, int idx[4], double w[4], double d[4],
+                          double s[4]) {
+    double u = ((double)(float)x - x0) * ih, top = n - 1;
+    int inside = u >= 0.0 && u <= top;
+    if (u != u) u = 0.0;
+    if (u < 0.0) u = 0.0;
+    if (u > top) u = top;
+    int i = (int)floor(u);
+    if (i > n - 2) i = n - 2;
+    orc_cr_basis(u - i, w, d, s);
+    for (int k = 0; k < 4; ++k) {
+        int q = i - 1 + k;
+        idx[k] = q < 0 ? 0 : (q > n - 1 ? n - 1 : q);
+        d[k] *= inside ? ih : 0.0;
+        s[k] *= inside ? ih * ih : 0.0;
+    }
+}
+
+static orc_jet orc_grid_jet(const orc_factor* f, const float* grid, double x, double y) {
+    const float* p = f->p;
+    int nx = (int)p[4], ny = (int)p[5];
+    const float* g = grid + (int64_t)p[6];
+    int ix[4], iy[4];
+    double wx[4], dx[4], sx[4], wy[4], dy[4], sy[4];
+    orc_grid_axis(x, p[0], p[2], nx, ix, wx, dx, sx);
+    orc_grid_axis(y, p[1], p[3], ny, iy, wy, dy, sy);
+    orc_jet j = {0, 0, 0, 0};
+    for (int b = 0; b < 4; ++b) {
+        double rv = 0, rd = 0, rs = 0;
+        for (int a = 0; a < 4; ++a) {
+            double v = g[(int64_t)iy[b] * nx + ix[a]];
+            rv += wx[a] * v; rd += dx[a] * v; rs += sx[a] * v;
+        }
+        j.v += wy[b] * rv; j.gx += wy[b] * rd; j.gy += dy[b] * rv; j.l += wy[b] * rs + sy[b] * rv;
+    }
+    return j;
+}
+
+static orc_jet orc_factor_jet(const orc_factor* f, const float* grid, double x, double y) {
     const float* p = f->p;
     orc_jet j = {0, 0, 0, 0};
     switch (f->kind) {
@@ -342,6 +395,10 @@ static orc_jet orc_factor_jet(const orc_factor* f, double x, double y) {
         j.v = (dx * dx + dy * dy <= p[2]) ? 1.0 : 0.0;
         break;
     }
+    case 9: /* tabulated (Catmull-Rom bicubic) */
+        if (!grid) { j.v = NAN; break; }
+        j = orc_grid_jet(f, grid, x, y);
+        break;
     default:
         j.v = NAN;
     }
@@ -355,7 +412,7 @@ static orc_jet orc_field_jet(const orc_field* f, double x, double y) {
         const orc_term* tm = &f->terms[t];
         orc_jet pr = {tm->coef, 0, 0, 0};
         for (int k = 0; k < tm->n_factors; ++k) {
-            orc_jet q = orc_factor_jet(&f->factors[tm->first_factor + k], x, y);
+            orc_jet q = orc_factor_jet(&f->factors[tm->first_factor + k], f->grid, x, y);
             orc_jet r;
             r.v = pr.v * q.v;
             r.gx = pr.v * q.gx + q.v * pr.gx;

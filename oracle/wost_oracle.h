@@ -35,6 +35,7 @@ typedef struct {
     const orc_term* terms; int32_t n_terms;
     const orc_factor* factors; int32_t n_factors;
     int32_t flags;     /* 1 = alpha detached (sigma' = sigma/alpha) */
+    const float* grid; int64_t n_grid;   /* kind-9 (tabulated) factor values */
 } orc_field;
 
 typedef struct {

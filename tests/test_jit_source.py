@@ -26,15 +26,42 @@ def test_generated_sources_name_their_variant():
     assert "walk_body<false, false, false, false, false>" in lap
 
 
+def _tabulated_source():
+    """A delta-tracking problem whose alpha and source are tabulated (WOST_FK_GRID)."""
+    import numpy as np
+
+    from dcrmontecarlo_amd import fields as F
+    from dcrmontecarlo_amd.geometry import PolyLinesSimple
+    from dcrmontecarlo_amd.solvers.WoStSolver import kernel_source
+
+    sc = S.variable_coefficients()
+    xs = np.linspace(-1.6, 1.6, 33, dtype=np.float32)
+    a = F.tabulated(1.0 + 0.1 * np.add.outer(xs, xs) ** 2, -1.6, -1.6, 0.1, 0.1)
+    f = F.tabulated(np.outer(xs, xs), -1.6, -1.6, 0.1, 0.1) * F.indicator_disk((0, 0), 1.5)
+    return kernel_source(PolyLinesSimple(sc.dirichlet), sc.g, PolyLinesSimple(sc.neumann), source=f,
+                         sigma=sc.sigma, alpha=a)
+
+
+def test_tabulated_fields_are_generated():
+    src = _tabulated_source()
+    assert src.count("wost::fj_grid(grid + ") == 1 and "wost::fv_grid(grid + 0," in src
+    assert "reinterpret_cast<const float*>(A.prog + " in src
+
+
 def test_generated_sources_compile_for_gfx950():
-    names = ["laplace_square", "poisson_square", "variable_coefficients", "dcr_dipole", "wenner_topography"]
+    names = ["laplace_square", "poisson_square", "variable_coefficients", "dcr_dipole", "wenner_topography",
+             "tabulated"]
     with tempfile.TemporaryDirectory() as d:
         procs = []
         for n in names:
-            sc = S.ALL[n]() if n != "wenner_topography" else S.wenner_topography(n_electrodes=4, n_walks=1)
+            if n == "tabulated":
+                src = _tabulated_source()
+            else:
+                sc = S.ALL[n]() if n != "wenner_topography" else S.wenner_topography(n_electrodes=4, n_walks=1)
+                src = sc.kernel_source()
             path = os.path.join(d, n + ".hip")
             with open(path, "w") as f:
-                f.write(sc.kernel_source())
+                f.write(src)
             procs.append((n, subprocess.Popen(
                 ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "--cuda-device-only", "-c", *HIPRTC_OPTS,
                  "-I" + CSRC, "-I" + os.path.join(REPO, "include"), path, "-o", path + ".o"],
