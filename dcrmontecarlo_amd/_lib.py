@@ -23,6 +23,7 @@ WOST_ERR_OOM = -5
 
 ABI_VERSION = 2   # include/wost.h WOST_ABI_VERSION
 WOST_BLOCK_WALKS = 4096
+WOST_MAX_SOURCES = 16   # include/wost.h
 WOST_SAMPLER_TABLE_N = 4097
 COMPAT = {"reference": 0, "fixed": 1}
 SLOT_BOUNDARY, SLOT_SOURCE = 0, 1
@@ -86,6 +87,10 @@ def _load():
                                  POINTER(c_uint32)]),
         "wost_solve_history": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int32, c_float, c_uint64,
                                          POINTER(c_double), POINTER(c_float), POINTER(c_uint32), POINTER(c_float)]),
+        "wost_set_sources": (c_int32, [H, POINTER(POINTER(WostField)), c_int32]),
+        "wost_solve_multi": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
+                                       c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_float),
+                                       POINTER(c_uint32)]),
         "wost_last_timing": (c_int32, [H, POINTER(WostTiming)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),

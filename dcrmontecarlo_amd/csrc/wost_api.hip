@@ -119,12 +119,13 @@ struct Program {
     }
 };
 
+// f: N_FIELDS fields (absent ones empty)
 void build_program(const HostField* f, double sigma_bar, Program& out) {
     DProgram hdr{};
     std::vector<DTerm> terms;
     std::vector<DFactor> factors;
     std::vector<float> grid;
-    for (int s = 0; s < N_SLOTS; ++s) {
+    for (int s = 0; s < N_FIELDS; ++s) {
         hdr.field[s].present = f[s].present ? 1 : 0;
         hdr.field[s].flags = f[s].flags;
         hdr.field[s].first_term = (int)terms.size();
@@ -178,7 +179,8 @@ struct wost_handle {
     int compat = WOST_COMPAT_REFERENCE;
     int num_cus = 0;
     std::vector<float> dverts, nverts;
-    HostField fields[N_SLOTS];
+    HostField fields[N_FIELDS];   // N_SLOTS problem fields, then sources 1.. of wost_set_sources
+    int n_sources = 1;
     bool delta = false;
     double sigma_bar = 0.0;
     Program prog;
@@ -213,7 +215,7 @@ struct wost_handle {
     unsigned long long* d_counter = nullptr;
     float* d_val = nullptr;
     uint32_t* d_steps = nullptr;
-    int64_t ws_cap = 0;
+    int64_t ws_cap = 0, ws_val_cap = 0;
     int64_t* d_begin = nullptr;
     int64_t begin_cap = 0;
     double* d_bstats = nullptr;
@@ -245,16 +247,16 @@ int upload_program(wost_handle* h) {
 // The field-specialised kernel for `mode` (with the walk recorder compiled in
 // when `record`), or nullptr when it is disabled or could not be built (the
 // precompiled kernel is used then; same results).
-hipFunction_t jit_kernel(wost_handle* h, int mode, bool record) {
+hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1) {
     if (!h->jit_enabled) return nullptr;
-    const int key = 2 * mode + (record ? 1 : 0);
+    const int key = (2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns;
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
     h->jit_mode = key;
     h->jit_version = h->prog_version;
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
                                          (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2),
-                                         record);
+                                         record, ns);
     std::string err;
     hipFunction_t fn = nullptr;
     if (!jit_get_kernel(h->device, src, &fn, &err)) {
@@ -357,17 +359,19 @@ int ensure_cap(T*& p, int64_t& cap, int64_t need) {
 }
 
 // per-walk value and step buffers, always of equal capacity
-int ensure_workspace(wost_handle* h, int64_t need) {
-    if (need <= h->ws_cap && h->d_val && h->d_steps) return WOST_OK;
+// Per-walk results of `need` walks with `ns` values each.
+int ensure_workspace(wost_handle* h, int64_t need, int ns = 1) {
+    if (need <= h->ws_cap && need * ns <= h->ws_val_cap && h->d_val && h->d_steps) return WOST_OK;
     if (h->d_val) (void)hipFree(h->d_val);
     if (h->d_steps) (void)hipFree(h->d_steps);
     h->d_val = nullptr;
     h->d_steps = nullptr;
-    h->ws_cap = 0;
-    hipError_t e = hipMalloc(&h->d_val, sizeof(float) * (size_t)need);
+    h->ws_cap = h->ws_val_cap = 0;
+    hipError_t e = hipMalloc(&h->d_val, sizeof(float) * (size_t)need * (size_t)ns);
     if (e == hipSuccess) e = hipMalloc(&h->d_steps, sizeof(uint32_t) * (size_t)need);
     if (e != hipSuccess) return fail(WOST_ERR_OOM, "per-walk workspace of %lld walks: %s", (long long)need, hipGetErrorString(e));
     h->ws_cap = need;
+    h->ws_val_cap = need * ns;
     return WOST_OK;
 }
 
@@ -548,6 +552,10 @@ int wost_set_field(wost_handle* h, int32_t slot, const wost_field* field) {
     int rc = convert_field(field, hf, s == SLOT_G ? "boundary" : "source");
     if (rc != WOST_OK) return rc;
     h->fields[s] = hf;
+    if (s == SLOT_F) {   // setSourceTerm: back to a single source
+        for (int k = SLOT_EXTRA; k < N_FIELDS; ++k) h->fields[k] = HostField();
+        h->n_sources = 1;
+    }
     h->prog_dirty = true;
     HIP_TRY(hipSetDevice(h->device));
     return upload_program(h);
@@ -587,8 +595,12 @@ constexpr int64_t kMaxRecordBatchBytes = int64_t(1) << 30;   // device buffer of
 // (wost_solve_history): records[walk][max_steps + 1][kRecFloats] on the host.
 int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W, int64_t block_begin,
                int64_t block_end, int32_t max_steps, float eps, uint64_t seed, double* block_stats,
-               double* point_stats, float* walk_values, uint32_t* walk_steps, float* records) {
+               double* point_stats, float* walk_values, uint32_t* walk_steps, float* records, bool multi = false) {
     if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    const int ns = h->n_sources;
+    if (ns != 1 && !multi)
+        return fail(WOST_ERR_INVALID_ARG, "the handle has %d sources (wost_set_sources): use wost_solve_multi", ns);
+    const int row = 2 * ns + 1;   // doubles per block / point row
     if (n_points < 0 || (n_points > 0 && !points)) return fail(WOST_ERR_INVALID_ARG, "bad points");
     if (W <= 0) return fail(WOST_ERR_INVALID_ARG, "nWalks must be >= 1 (got %lld)", (long long)W);
     if (max_steps < 0) return fail(WOST_ERR_INVALID_ARG, "maxSteps must be >= 0");
@@ -617,7 +629,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
 
     h->timing = wost_timing{};
     const int64_t nblk = block_end - block_begin;
-    if (point_stats) std::fill(point_stats, point_stats + 3 * n_points, 0.0);
+    if (point_stats) std::fill(point_stats, point_stats + row * n_points, 0.0);
     if (nblk == 0) return WOST_OK;
 
     // block -> global walk range
@@ -629,7 +641,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
 
     const int64_t walks_total = blk_end(block_end - 1) - blk_begin(block_begin);
     // walks per launch: the recorder's device buffer bounds it
-    int64_t batch_limit = kMaxBatchWalks;
+    int64_t batch_limit = kMaxBatchWalks / ns;
     const int64_t rec_stride = (int64_t)max_steps + 1;
     const int64_t rec_walk_bytes = rec_stride * kRecFloats * (int64_t)sizeof(float);
     if (records) {
@@ -641,8 +653,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     }
     if ((rc = ensure_cap(h->d_points, h->points_cap, std::max<int64_t>(n_points, 1))) != WOST_OK) return rc;
     HIP_TRY(hipMemcpyAsync(h->d_points, points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
-    if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, batch_limit))) != WOST_OK) return rc;
-    if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * 3)) != WOST_OK) return rc;
+    if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, batch_limit), ns)) != WOST_OK) return rc;
+    if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * row)) != WOST_OK) return rc;
     float* d_rec = nullptr;
     struct RecFree {
         float*& p;
@@ -650,7 +662,10 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     } rec_free{d_rec};
     if (records) HIP_TRY(hipMalloc(&d_rec, (size_t)std::min<int64_t>(walks_total, batch_limit) * rec_walk_bytes));
 
-    const hipFunction_t jfn = jit_kernel(h, mode, records != nullptr);
+    const hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns);
+    if (ns > 1 && !jfn)
+        return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
+                    h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
     const size_t lds = walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points);
     int blocks_per_cu = 0;
     if (jfn)
@@ -733,10 +748,12 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
             HIP_TRY(launch_walk(mode, a, grid, h->stream));
         }
         HIP_TRY(hipEventRecord(h->ev[1], h->stream));
-        HIP_TRY(launch_block_reduce(h->d_val, h->d_steps, h->d_begin, nb, h->d_bstats + 3 * (j - block_begin), h->stream));
+        HIP_TRY(launch_block_reduce(h->d_val, h->d_steps, h->d_begin, nb, ns, h->d_bstats + row * (j - block_begin),
+                                    h->stream));
         HIP_TRY(hipEventRecord(h->ev[2], h->stream));
         if (walk_values)
-            HIP_TRY(hipMemcpyAsync(walk_values + walks_done, h->d_val, sizeof(float) * count, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipMemcpyAsync(walk_values + walks_done * ns, h->d_val, sizeof(float) * count * ns,
+                                   hipMemcpyDeviceToHost, h->stream));
         if (walk_steps)
             HIP_TRY(hipMemcpyAsync(walk_steps + walks_done, h->d_steps, sizeof(uint32_t) * count, hipMemcpyDeviceToHost, h->stream));
         if (records)
@@ -752,8 +769,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         walks_done += count;
         j = j2;
     }
-    std::vector<double> bs(3 * nblk);
-    HIP_TRY(hipMemcpyAsync(bs.data(), h->d_bstats, sizeof(double) * 3 * nblk, hipMemcpyDeviceToHost, h->stream));
+    std::vector<double> bs(row * nblk);
+    HIP_TRY(hipMemcpyAsync(bs.data(), h->d_bstats, sizeof(double) * row * nblk, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipEventRecord(h->ev[5], h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     float tt = 0.f;
@@ -761,15 +778,13 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
 
     uint64_t steps_sum = 0;
     for (int64_t b = 0; b < nblk; ++b) {
-        steps_sum += (uint64_t)bs[3 * b + 2];
+        steps_sum += (uint64_t)bs[row * b + row - 1];
         if (point_stats) {
             const int64_t p = (block_begin + b) / nbpp;
-            point_stats[3 * p + 0] += bs[3 * b + 0];
-            point_stats[3 * p + 1] += bs[3 * b + 1];
-            point_stats[3 * p + 2] += bs[3 * b + 2];
+            for (int c = 0; c < row; ++c) point_stats[row * p + c] += bs[row * b + c];
         }
     }
-    if (block_stats) std::memcpy(block_stats, bs.data(), sizeof(double) * 3 * nblk);
+    if (block_stats) std::memcpy(block_stats, bs.data(), sizeof(double) * row * nblk);
     h->timing.walk_kernel_ms = walk_ms;
     h->timing.reduce_kernel_ms = red_ms;
     h->timing.total_ms = tt;
@@ -799,6 +814,39 @@ int wost_solve_history(wost_handle* h, const float* points, int64_t n_points, in
     const int64_t nb = wost_num_blocks(n_points, W);
     return solve_impl(h, points, n_points, W, 0, nb, max_steps, eps, seed, nullptr, point_stats, walk_values,
                       walk_steps, records);
+}
+
+int wost_solve_multi(wost_handle* h, const float* points, int64_t n_points, int64_t W, int64_t block_begin,
+                     int64_t block_end, int32_t max_steps, float eps, uint64_t seed, double* block_stats,
+                     double* point_stats, float* walk_values, uint32_t* walk_steps) {
+    return solve_impl(h, points, n_points, W, block_begin, block_end, max_steps, eps, seed, block_stats, point_stats,
+                      walk_values, walk_steps, nullptr, true);
+}
+
+int wost_set_sources(wost_handle* h, const wost_field* const* sources, int32_t n) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    if (n < 1 || n > WOST_MAX_SOURCES || !sources)
+        return fail(WOST_ERR_INVALID_ARG, "need 1..%d sources (got %d)", WOST_MAX_SOURCES, n);
+    std::vector<HostField> conv(n);
+    int64_t grid = 0;
+    for (int s = 0; s < n; ++s) {
+        if (!sources[s]) return fail(WOST_ERR_INVALID_ARG, "source %d is NULL", s);
+        char name[32];
+        std::snprintf(name, sizeof(name), "source[%d]", s);
+        int rc = convert_field(sources[s], conv[s], name);
+        if (rc != WOST_OK) return rc;
+        grid += (int64_t)conv[s].grid.size();
+    }
+    for (int s = 0; s < N_SLOTS; ++s)
+        if (s != SLOT_F) grid += (int64_t)h->fields[s].grid.size();
+    if (grid >= (int64_t(1) << 24))
+        return fail(WOST_ERR_INVALID_ARG, "tabulated fields hold %lld values together (limit 2^24)", (long long)grid);
+    h->fields[SLOT_F] = conv[0];
+    for (int s = 1; s < WOST_MAX_SOURCES; ++s) h->fields[SLOT_EXTRA + s - 1] = s < n ? conv[s] : HostField();
+    h->n_sources = n;
+    h->prog_dirty = true;
+    HIP_TRY(hipSetDevice(h->device));
+    return upload_program(h);
 }
 
 

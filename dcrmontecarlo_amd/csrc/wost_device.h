@@ -115,9 +115,12 @@ struct alignas(16) DField {
 };
 
 // Program buffer header (uploaded once per handle, read with uniform indices).
-enum { SLOT_G = 0, SLOT_F = 1, SLOT_SIGMA = 2, SLOT_ALPHA = 3, N_SLOTS = 4 };
+// Slots 0-3 are the problem's fields; source k > 0 of a multi-source solve
+// (wost_set_sources) is slot SLOT_EXTRA + k - 1 (source 0 is SLOT_F).
+enum { SLOT_G = 0, SLOT_F = 1, SLOT_SIGMA = 2, SLOT_ALPHA = 3, N_SLOTS = 4, SLOT_EXTRA = 4,
+       N_FIELDS = N_SLOTS + WOST_MAX_SOURCES - 1 };
 struct alignas(16) DProgram {
-    DField field[N_SLOTS];
+    DField field[N_FIELDS];
     float cheb_a[kChebA];
     float cheb_b[kChebB];
     float sigma_bar;

@@ -192,7 +192,7 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
 }  // namespace
 
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
-                         const float* dverts, int nd, const float* nverts, int nn, bool record) {
+                         const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -210,6 +210,15 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << (fG.present ? value_body(fG, terms, factors) : "        return 0.0f;\n") << "    }\n";
     o << "    __device__ __forceinline__ float f(float x, float y) const {\n"
       << (fF.present ? value_body(fF, terms, factors) : "        return 0.0f;\n") << "    }\n";
+    if (n_sources > 1) {   // multi-source: every source's value, each with f()'s operation sequence
+        o << "    __device__ __forceinline__ void f_multi(float x, float y, float* out) const {\n";
+        for (int s = 0; s < n_sources; ++s) {
+            const DField& fs = hdr.field[s == 0 ? SLOT_F : SLOT_EXTRA + s - 1];
+            o << "        out[" << s << "] = [&]() {\n"
+              << (fs.present ? value_body(fs, terms, factors) : "        return 0.0f;\n") << "        }();\n";
+        }
+        o << "    }\n";
+    }
     o << "    __device__ __forceinline__ float sigma(float x, float y) const {\n"
       << (fS.present ? value_body(fS, terms, factors) : "        return 0.0f;\n") << "    }\n";
     o << "    __device__ __forceinline__ float alpha(float x, float y) const {\n"
@@ -263,7 +272,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
       << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
       << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
-      << ">(A, fld, smem);\n}\n";
+      << (n_sources > 1 ? ", " + std::to_string(n_sources) : std::string()) << ">(A, fld, smem);\n}\n";
     return o.str();
 }
 

@@ -25,9 +25,11 @@ constexpr int kJitMaxConstVertices = 16;
 // HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
 // (wost_internal.h WalkMode) with the fields of `prog` and short polylines
 // (Dirichlet dverts[2*nd], Neumann nverts[2*nn]) compiled in; `record`: the
-// kernel can record walks (return_history).
+// kernel can record walks (return_history); `n_sources` > 1: the walk scores
+// sources SLOT_F, SLOT_EXTRA.. (multi-source batching).
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
-                         const float* dverts, int nd, const float* nverts, int nn, bool record);
+                         const float* dverts, int nd, const float* nverts, int nn, bool record,
+                         int n_sources = 1);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

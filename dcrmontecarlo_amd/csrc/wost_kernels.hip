@@ -173,46 +173,52 @@ hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s) {
 // ---------------------------------------------------------------------------
 constexpr int kReduceBlock = 256;
 
+// ns values per walk (multi-source solves): for each its sum and sum of
+// squares, then the steps -- rows of 2*ns+1 doubles. The summation order is
+// the same for every ns, so source k's sums do not depend on the other sources.
 __global__ void __launch_bounds__(kReduceBlock)
 wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ steps,
-                  const int64_t* __restrict__ begin, int64_t nblocks, double* __restrict__ out) {
+                  const int64_t* __restrict__ begin, int64_t nblocks, int ns, double* __restrict__ out) {
     __shared__ double s_sum[kReduceBlock], s_sq[kReduceBlock], s_st[kReduceBlock];
+    const int row = 2 * ns + 1;
     for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
         const int64_t lo = begin[b], hi = begin[b + 1];
-        double s = 0.0, q = 0.0;
-        uint64_t st = 0;
-        for (int64_t i = lo + threadIdx.x; i < hi; i += kReduceBlock) {
-            const double v = (double)val[i];
-            s += v;
-            q += v * v;
-            st += steps[i];
-        }
-        s_sum[threadIdx.x] = s;
-        s_sq[threadIdx.x] = q;
-        s_st[threadIdx.x] = (double)st;
-        __syncthreads();
-        for (int h = kReduceBlock / 2; h > 0; h >>= 1) {
-            if ((int)threadIdx.x < h) {
-                s_sum[threadIdx.x] += s_sum[threadIdx.x + h];
-                s_sq[threadIdx.x] += s_sq[threadIdx.x + h];
-                s_st[threadIdx.x] += s_st[threadIdx.x + h];
+        for (int k = 0; k < ns; ++k) {
+            double s = 0.0, q = 0.0;
+            uint64_t st = 0;
+            for (int64_t i = lo + threadIdx.x; i < hi; i += kReduceBlock) {
+                const double v = (double)val[i * ns + k];
+                s += v;
+                q += v * v;
+                if (k == 0) st += steps[i];
+            }
+            s_sum[threadIdx.x] = s;
+            s_sq[threadIdx.x] = q;
+            s_st[threadIdx.x] = (double)st;
+            __syncthreads();
+            for (int h = kReduceBlock / 2; h > 0; h >>= 1) {
+                if ((int)threadIdx.x < h) {
+                    s_sum[threadIdx.x] += s_sum[threadIdx.x + h];
+                    s_sq[threadIdx.x] += s_sq[threadIdx.x + h];
+                    if (k == 0) s_st[threadIdx.x] += s_st[threadIdx.x + h];
+                }
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) {
+                out[row * b + 2 * k] = s_sum[0];
+                out[row * b + 2 * k + 1] = s_sq[0];
+                if (k == 0) out[row * b + row - 1] = s_st[0];
             }
             __syncthreads();
         }
-        if (threadIdx.x == 0) {
-            out[3 * b + 0] = s_sum[0];
-            out[3 * b + 1] = s_sq[0];
-            out[3 * b + 2] = s_st[0];
-        }
-        __syncthreads();
     }
 }
 
 hipError_t launch_block_reduce(const float* val, const uint32_t* steps, const int64_t* begin,
-                               int64_t nblocks, double* out, hipStream_t s) {
+                               int64_t nblocks, int ns, double* out, hipStream_t s) {
     if (nblocks <= 0) return hipSuccess;
     const int grid = (int)(nblocks < 65536 ? nblocks : 65536);
-    wost_block_reduce<<<grid, kReduceBlock, 0, s>>>(val, steps, begin, nblocks, out);
+    wost_block_reduce<<<grid, kReduceBlock, 0, s>>>(val, steps, begin, nblocks, ns, out);
     return hipGetLastError();
 }
 

@@ -81,11 +81,17 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // nn, x, y, dx, dy, r) (the interpreted kernels scan the staged vertices; the
 // specialised ones may have them compiled in). TREE: Neumann queries through
 // the segment tree. REC: the kernel can record walks (A.rec).
-template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, class F>
+// NS > 1 (multi-source batching): the walk scores NS source
+// fields at once -- the walk itself does not depend on the source, so every
+// source's total is bit for bit what a single-source solve of it gives. The
+// Fields policy then provides f_multi(x, y, float out[NS]); per-walk values go
+// to out_val[local walk * NS + k].
+template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
     // the walk's position updates round op by op like the reference (torch CPU
     // has no FMA contraction); the field math it calls keeps its own setting
 #pragma clang fp contract(off)
+    static_assert(NS >= 1 && (NS == 1 || SRC) && (NS == 1 || !REC), "multi-source walks need a source, no recorder");
     float2* sD = reinterpret_cast<float2*>(smem);
     float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
     float* sPhi = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
@@ -130,20 +136,24 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     float phi = 0.f;            // atan2 of currentNormal (:228), set when onB
     float w = 1.f;              // attenuation_coef
     float ax = 1.f;             // alpha(current_point), cached
-    float total = 0.f;          // this walk's contributions
+    float total[NS];            // this walk's contributions (one per source)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) total[s] = 0.f;
 
     for (;;) {
         // --- walk termination: while-condition of :206, boundary term :295-298
         if (active && !((k < A.max_steps) && (dD > A.eps))) {
             float g = fld.has_g() ? fld.g(px, py) : 0.0f;
             if (DELTA) g = g * w;
-            total = total + g;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) total[s] = total[s] + g;
             const int64_t li = (int64_t)(wid - (uint64_t)A.wid_begin);
             if (REC && A.rec != nullptr) {
                 float* rr = A.rec + ((size_t)li * (size_t)A.rec_stride + (size_t)k) * kRecFloats;
-                rr[REC_X] = px; rr[REC_Y] = py; rr[REC_C] = g; rr[REC_AUX] = total;   // end record
+                rr[REC_X] = px; rr[REC_Y] = py; rr[REC_C] = g; rr[REC_AUX] = total[0];   // end record
             }
-            A.out_val[li] = total;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) A.out_val[li * NS + s] = total[s];
             A.out_steps[li] = (uint32_t)k;
             active = false;
         }
@@ -179,7 +189,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 if (points_in_lds) q = sP[pid];
                 else q = A.points[pid];
                 px = q.x; py = q.y;
-                k = 0; dD = 1.0f; onB = false; phi = 0.f; w = 1.f; total = 0.f;
+                k = 0; dD = 1.0f; onB = false; phi = 0.f; w = 1.f;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) total[s] = 0.f;
                 if (DELTA) ax = fld.alpha(px, py);
                 active = true;
             }
@@ -245,16 +257,31 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 gnorm = inv_sb * (1.0f - fld.inv_i0(r * sqrt_sb));   // solvers/utils.py:43-44
                 aj = fld.alpha_jet(yx, yy);
             }
-            float c = 0.0f;
-            if (!clipped) {
-                const float f = fld.f(yx, yy);
-                if (DELTA)
-                    c = (f * gnorm) * f_rcp(f_sqrt(aj.v * ax)) * w;  // :253-254
-                else
-                    c = f * ((r * r) / 4.0f);                        // :256, utils.py:61
+            if constexpr (NS == 1) {
+                float c = 0.0f;
+                if (!clipped) {
+                    const float f = fld.f(yx, yy);
+                    if (DELTA)
+                        c = (f * gnorm) * f_rcp(f_sqrt(aj.v * ax)) * w;  // :253-254
+                    else
+                        c = f * ((r * r) / 4.0f);                        // :256, utils.py:61
+                }
+                total[0] = total[0] + c;                                 // :258
+                cv = c;
+            } else if (!clipped) {                                       // the same per source
+                float fv[NS];
+                fld.f_multi(yx, yy, fv);
+                const float sa = DELTA ? f_rcp(f_sqrt(aj.v * ax)) : 0.0f;
+                const float q = DELTA ? 0.0f : ((r * r) / 4.0f);
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    const float c = DELTA ? ((fv[s] * gnorm) * sa * w) : fv[s] * q;
+                    total[s] = total[s] + c;
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < NS; ++s) total[s] = total[s] + 0.0f;
             }
-            total = total + c;                                       // :258
-            cv = c;
         }
         if (REC && A.rec != nullptr) {                               // :218-222, :261-266
             // the tree's silhouette distance is exact only below dD: recompute it

@@ -334,6 +334,76 @@ class WostSolver_2D:
         self.last_timing = self.timing()
         return wv.reshape(n, nWalks), ws.reshape(n, nWalks)
 
+    # ---- multi-source batching -------------------------------
+    def _solve_sources(self, solvePoints, sources, nWalks, maxSteps, eps, seed, want_walks):
+        p = _points_np(solvePoints)
+        n = p.shape[0]
+        nWalks = int(nWalks)
+        if nWalks < 1:
+            raise ValueError("nWalks must be >= 1")
+        srcs = list(sources)
+        if not srcs:
+            raise ValueError("sources must hold at least one source field")
+        fields = [self._conv(0.0 if f is None else f, f"sources[{k}]") for k, f in enumerate(srcs)]
+        nb = self.num_blocks(n, nWalks)
+        sums, vals, steps = [], [], None
+        try:
+            for c0 in range(0, len(fields), _lib.WOST_MAX_SOURCES):
+                chunk = fields[c0:c0 + _lib.WOST_MAX_SOURCES]
+                S = len(chunk)
+                packed = [_lib.make_field(f) for f in chunk]
+                arr = (ctypes.POINTER(_lib.WostField) * S)(*[ctypes.pointer(wf) for wf, _ in packed])
+                _lib.check(_lib.lib.wost_set_sources(self._h, arr, S), "WostSolver_2D.solve_sources")
+                s = np.zeros((n, 2 * S + 1), np.float64)
+                wv = np.empty(n * nWalks * S, np.float32) if want_walks else None
+                ws = np.empty(n * nWalks, np.uint32) if want_walks else None
+                _lib.check(_lib.lib.wost_solve_multi(self._h, _lib.fptr(p), n, nWalks, 0, nb, int(maxSteps),
+                                                     float(eps), int(seed) & (2**64 - 1), None, _lib.dptr(s),
+                                                     _lib.fptr(wv), _lib.u32ptr(ws)), "WostSolver_2D.solve_sources")
+                self.last_timing = self.timing()
+                sums.append(s)
+                if want_walks:
+                    vals.append(wv.reshape(n, nWalks, S).transpose(2, 0, 1))
+                    steps = ws.reshape(n, nWalks)
+        finally:   # back to the solver's own (single) source
+            wf, keep = _lib.make_field(self.source)
+            _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_SOURCE, ctypes.pointer(wf) if wf else None),
+                       "WostSolver_2D.solve_sources")
+        return sums, vals, steps
+
+    def solve_sources(self, solvePoints, sources, nWalks=1000, maxSteps=1000, eps=1e-4, *, seed: int = 0,
+                      return_stats: bool = False):
+        """Multi-source batching (beyond the reference, which solves one source per
+        solve): u[k] is the solve of this problem with source ``sources[k]``
+        (fields, numbers or callables), all scored by the same walks. The walks
+        do not depend on f (solvers/WoStSolver.py:242-258), so each u[k] is bit for
+        bit ``setSourceTerm(sources[k]); solve(...)`` with the same seed, at about
+        the cost of one solve (16 sources per launch; more are batched in groups).
+        Returns float32 [S, N]; with ``return_stats`` also a SolveStats whose mean
+        and stderr are [S, N]. The solver's own source is restored afterwards."""
+        sums, _, _ = self._solve_sources(solvePoints, sources, nWalks, maxSteps, eps, seed, False)
+        stats = [st for s in sums for st in _stats_of_multi(s, int(nWalks))]
+        u = np.stack([st.mean.astype(np.float32) for st in stats])
+        if not return_stats:
+            return u
+        t = self.last_timing
+        return u, SolveStats(mean=np.stack([st.mean for st in stats]), stderr=np.stack([st.stderr for st in stats]),
+                             mean_steps=stats[0].mean_steps, walks=stats[0].walks, total_steps=stats[0].total_steps,
+                             kernel_ms=t["walk_kernel_ms"], total_ms=t["total_ms"])
+
+    def solve_sources_walks(self, solvePoints, sources, nWalks=1000, maxSteps=1000, eps=1e-4, *, seed: int = 0):
+        """Per-walk values of every source, float32 [S, N, nWalks], and the walks'
+        step counts, uint32 [N, nWalks] (shared by all sources)."""
+        _, vals, steps = self._solve_sources(solvePoints, sources, nWalks, maxSteps, eps, seed, True)
+        return np.concatenate(vals, axis=0), steps
+
+
+def _stats_of_multi(sums: np.ndarray, n_walks: int):
+    """SolveStats of each source from [N, 2S+1] wost_solve_multi rows."""
+    S = (sums.shape[1] - 1) // 2
+    return [stats_from_sums(np.stack([sums[:, 2 * k], sums[:, 2 * k + 1], sums[:, -1]], axis=1), n_walks)
+            for k in range(S)]
+
 
 def _history(rec, wv, ws, n, nWalks, has_neumann, has_source, as_torch):
     """The reference's history_dict (solvers/WoStSolver.py:180-309) from the recorder's

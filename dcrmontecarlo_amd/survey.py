@@ -17,6 +17,7 @@ data:
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 
 import numpy as np
@@ -35,6 +36,26 @@ def wenner_quadripoles(n_electrodes: int, a: int = 1) -> np.ndarray:
     """[(A, M, N, B)] Wenner-alpha quadripoles with electrode spacing a (in electrode steps)."""
     i = np.arange(n_electrodes - 3 * a)
     return np.stack([i, i + a, i + 2 * a, i + 3 * a], axis=1)
+
+
+def dipole_dipole_quadripoles(n_electrodes: int, n_max: int = 4) -> np.ndarray:
+    """[(A, B, M, N)] dipole-dipole quadripoles: current dipole (c, c+1), potential
+    dipole (c+1+n, c+2+n) for separations n = 1..n_max (rows ordered by c, then n)."""
+    rows = [(c, c + 1, c + 1 + n, c + 2 + n) for c in range(n_electrodes) for n in range(1, n_max + 1)
+            if c + 2 + n < n_electrodes]
+    return np.array(rows, dtype=np.int64).reshape(-1, 4)
+
+
+def electrode_source(position, width: float, current: float = 1.0) -> F.Field:
+    """Current injection at an electrode: a normalised Gaussian of standard deviation
+    ``width`` (the reference's dcr_current_source form, tests/testGeophysicalScenario.py:11-33)."""
+    norm = current / (2.0 * math.pi * width * width)
+    return norm * F.gaussian((float(position[0]), float(position[1])), width)
+
+
+def dipole_source(a, b, width: float, current: float = 1.0) -> F.Field:
+    """+current at electrode position a, -current at b (notebook cell 17's dipole)."""
+    return electrode_source(a, width, current) - electrode_source(b, width, current)
 
 
 @dataclass
@@ -108,3 +129,53 @@ def compare(a: ApparentResistivity, b: ApparentResistivity) -> dict:
     d = a.rho_a[ok] - b.rho_a[ok]
     return {"rmse": float(np.sqrt(np.mean(d * d))), "mc_1sigma": float(np.sqrt(np.mean(b.se[ok] ** 2))),
             "resolved": int(ok.sum())}
+
+
+@dataclass
+class MultiSurveyResult:
+    quadripoles: np.ndarray   # [Q, 4] (A, B, M, N)
+    model: DipoleData         # [Q]
+    background: DipoleData    # [Q]
+    rho: ApparentResistivity  # [Q]
+    u_model: np.ndarray       # [T, E] potential at every electrode for each transmitter dipole
+    u_background: np.ndarray  # [T, E]
+    transmitters: np.ndarray  # [T, 2] (A, B) of each row of u_*
+    walk_steps: int
+
+
+def run_dipole_dipole_survey(sc: Scenario, alpha_bg: float, n_walks: int, n_max: int = 4, width: float = 0.5,
+                             seed: int = 0, device: int | None = None, solvers=None) -> MultiSurveyResult:
+    """A full dipole-dipole pseudosection: one transmitter dipole (c, c+1) per
+    electrode pair, every electrode's potential for each, model and homogeneous
+    background. All transmitters are scored by the same walks
+    (WostSolver_2D.solve_sources: the walks do not depend on the source), so the
+    survey costs two walk sets per electrode instead of two per transmitter."""
+    E = len(sc.points)
+    quad = dipole_dipole_quadripoles(E, n_max)
+    tx = np.unique(quad[:, :2], axis=0) if len(quad) else np.zeros((0, 2), np.int64)
+    srcs = [dipole_source(sc.points[a], sc.points[b], width) for a, b in tx]
+    if solvers is None:
+        solvers = (sc.solver(device=device), homogeneous(sc, alpha_bg).solver(device=device))
+    sm, sh = solvers
+    out = []
+    steps = 0
+    for s in (sm, sh):
+        if not srcs:
+            out.append((np.zeros((0, E)), np.zeros((0, E))))
+            continue
+        _, st = s.solve_sources(sc.points, srcs, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=seed,
+                                return_stats=True)
+        out.append((st.mean, st.stderr))
+        steps += st.total_steps
+    row = {(int(a), int(b)): k for k, (a, b) in enumerate(tx)}
+    t = np.array([row[(int(a), int(b))] for a, b, _, _ in quad], dtype=np.int64)
+
+    def dd(mean, se):
+        if not len(quad):
+            return DipoleData(np.zeros(0), np.zeros(0))
+        m, n = quad[:, 2], quad[:, 3]
+        return DipoleData(mean[t, m] - mean[t, n], np.sqrt(se[t, m] ** 2 + se[t, n] ** 2))
+
+    dm, dh = dd(*out[0]), dd(*out[1])
+    return MultiSurveyResult(quad, dm, dh, apparent_resistivity(dm, dh, 1.0 / alpha_bg), out[0][0], out[1][0], tx,
+                             steps)

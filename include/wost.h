@@ -32,6 +32,9 @@ extern "C" {
 
 #define WOST_ABI_VERSION 2
 
+/* Most source fields one multi-source solve can score (wost_set_sources). */
+#define WOST_MAX_SOURCES 16
+
 /* Walks of one query point are grouped in blocks of this many consecutive
  * walk indices. Per-block partial sums are the unit of reduction and of
  * multi-GPU sharding (a shard is a contiguous range of blocks), which makes
@@ -223,6 +226,27 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points,
 int wost_solve_history(wost_handle* h, const float* points, int64_t n_points,
                        int64_t walks_per_point, int32_t max_steps, float eps, uint64_t seed,
                        double* point_stats, float* walk_values, uint32_t* walk_steps, float* records);
+
+/* Multi-source batching (beyond the reference, which solves
+ * one source per WostSolver_2D.solve): a DC survey injects current through
+ * many electrode pairs, each a different source f. The walks do not depend on
+ * f (it only weights the source samples, solvers/WoStSolver.py:242-258), so one
+ * walk can score every source at once. wost_set_sources replaces the
+ * handle's source by n_sources fields (1 <= n <= WOST_MAX_SOURCES; sources[0]
+ * takes the place of setSourceTerm's field). wost_solve_multi then solves
+ * like wost_solve, with per-source results:
+ *   block_stats [n_blocks_in_range][2*S+1], point_stats [n_points][2*S+1]:
+ *       (sum_0, sumsq_0, ..., sum_{S-1}, sumsq_{S-1}, steps)
+ *   walk_values [walks][S], walk_steps [walks]
+ * Each source's sums are bit for bit those of a single-source solve of that
+ * source with the same seed. Needs the field-specialised (hiprtc) kernel when
+ * S > 1. wost_solve and wost_solve_history need S == 1. */
+int wost_set_sources(wost_handle* h, const wost_field* const* sources, int32_t n_sources);
+int wost_solve_multi(wost_handle* h, const float* points, int64_t n_points,
+                     int64_t walks_per_point, int64_t block_begin, int64_t block_end,
+                     int32_t max_steps, float eps, uint64_t seed,
+                     double* block_stats, double* point_stats,
+                     float* walk_values, uint32_t* walk_steps);
 
 int wost_last_timing(const wost_handle* h, wost_timing* out);
 

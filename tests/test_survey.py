@@ -92,3 +92,21 @@ def test_gpu_survey_rho_a_matches_cpu_oracle(gpu_available):
     # the background survey's own rho_a vs the model's is a different quantity: the
     # resistive/conductive bodies must move rho_a away from rho_bg somewhere
     assert np.nanmax(np.abs(res.rho.rho_a[res.rho.resolved] - 0.01)) > 0.0
+
+
+def test_dipole_dipole_quadripoles():
+    q = survey.dipole_dipole_quadripoles(6, n_max=2)
+    assert q.tolist() == [[0, 1, 2, 3], [0, 1, 3, 4], [1, 2, 3, 4], [1, 2, 4, 5], [2, 3, 4, 5]]
+    assert survey.dipole_dipole_quadripoles(3).shape == (0, 4)
+
+
+def test_dipole_source_is_antisymmetric_and_normalised():
+    f = survey.dipole_source((-3.0, 0.0), (3.0, 0.0), 0.5)
+    x = np.linspace(-8, 8, 641)
+    X, Y = np.meshgrid(x, x)
+    v = f(np.stack([X.ravel(), Y.ravel()], 1)).reshape(X.shape)
+    v = np.asarray(v, np.float64)
+    np.testing.assert_allclose(v, -v[:, ::-1], atol=1e-6)
+    h = x[1] - x[0]
+    pos = np.where(X < 0, v, 0).sum() * h * h
+    assert pos == pytest.approx(1.0, rel=1e-3)
