@@ -92,6 +92,7 @@ def _load():
                                        c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_float),
                                        POINTER(c_uint32)]),
         "wost_last_timing": (c_int32, [H, POINTER(WostTiming)]),
+        "wost_greens_norm": (c_int32, [c_double, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
         "wost_kernel_source": (c_int32, [POINTER(WostProblem), ctypes.c_char_p, c_int64, POINTER(c_int64)]),
@@ -102,7 +103,11 @@ def _load():
                                           POINTER(c_uint8)]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        # an older build may lack a newer entry point: it loads, and calling the
+        # missing one raises AttributeError (the export test checks a fresh build)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
         fn.restype = res
         fn.argtypes = args
     if lib.wost_version() != ABI_VERSION:

@@ -142,7 +142,6 @@ void build_program(const HostField* f, double sigma_bar, Program& out) {
         }
         grid.insert(grid.end(), f[s].grid.begin(), f[s].grid.end());
     }
-    fit_i0e_chebyshev(hdr.cheb_a, kChebA, hdr.cheb_b, kChebB);
     hdr.sigma_bar = (float)sigma_bar;
     hdr.sqrt_sigma_bar = (float)std::sqrt(sigma_bar > 0 ? sigma_bar : 0.0);
     hdr.inv_sigma_bar = sigma_bar > 0 ? (float)(1.0 / sigma_bar) : 0.f;
@@ -271,13 +270,17 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1) {
 
 int ensure_table(wost_handle* h) {
     if (h->table_ready) return WOST_OK;
-    h->table.assign(WOST_SAMPLER_TABLE_N, 0.f);
-    if (h->delta)
+    // sampler nodes, then (delta tracking) the G_norm cells (wost_device.h)
+    const size_t n = table_floats(h->delta);
+    h->table.assign(n, 0.f);
+    if (h->delta) {
         screened_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N, h->sigma_bar);
-    else
+        greens_norm_cells(h->table.data() + kSamplerFloatsPadded, kGnormCells, (double)kGnormCells / kGnormInvH);
+    } else {
         greens_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N);
-    if (!h->d_table) HIP_TRY(hipMalloc(&h->d_table, sizeof(float) * WOST_SAMPLER_TABLE_N));
-    HIP_TRY(hipMemcpy(h->d_table, h->table.data(), sizeof(float) * WOST_SAMPLER_TABLE_N, hipMemcpyHostToDevice));
+    }
+    if (!h->d_table) HIP_TRY(hipMalloc(&h->d_table, sizeof(float) * table_floats(true)));
+    HIP_TRY(hipMemcpy(h->d_table, h->table.data(), sizeof(float) * n, hipMemcpyHostToDevice));
     h->table_ready = true;
     return WOST_OK;
 }
@@ -576,6 +579,20 @@ int wost_sampler_table(const wost_handle* hc, float* out, int32_t n) {
     int rc = ensure_table(h);
     if (rc != WOST_OK) return rc;
     std::memcpy(out, h->table.data(), sizeof(float) * WOST_SAMPLER_TABLE_N);
+    return WOST_OK;
+}
+
+int wost_greens_norm(double sigma_bar, const float* radii, int64_t n, float* out) {
+    if (!(sigma_bar > 0.0) || n < 0 || (n > 0 && (!radii || !out)))
+        return fail(WOST_ERR_INVALID_ARG, "need sigma_bar > 0 and n >= 0 radii");
+    std::vector<float4> cells(kGnormCells);
+    greens_norm_cells(reinterpret_cast<float*>(cells.data()), kGnormCells, (double)kGnormCells / kGnormInvH);
+    // the kernels' constants (build_program)
+    const float sqrt_sb = (float)std::sqrt(sigma_bar), inv_sb = (float)(1.0 / sigma_bar);
+    for (int64_t i = 0; i < n; ++i) {
+        const float r = radii[i];
+        out[i] = greens_norm_from_table(cells.data(), r * sqrt_sb, r, inv_sb);
+    }
     return WOST_OK;
 }
 

@@ -22,12 +22,18 @@
 #define WOST_HD __host__ __device__ __forceinline__
 #define WOST_INF __builtin_inff()
 #define WOST_NAN __builtin_nanf("")
+// "does any lane of the wave need this": guards rare exact fallbacks so that
+// a wave skips them unless one of its lanes needs one (the host build of the
+// header tests the lane's own condition)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define WOST_ANY(c) __any(c)
+#else
+#define WOST_ANY(c) (c)
+#endif
 
 namespace wost {
 
 constexpr float kPiF = 3.14159265358979323846f;
-constexpr int kChebA = 17;   // i0e on [0,8], t = x/4 - 1           (max rel. error 5e-7 in float)
-constexpr int kChebB = 8;    // sqrt(x) i0e(x) on (8,inf), t = 16/x - 1 (max rel. error 2e-7 in float)
 
 // ---------------------------------------------------------------------------
 // Counter-based RNG: Philox4x32-10 (Salmon et al., SC'11), the bijection of
@@ -121,8 +127,6 @@ enum { SLOT_G = 0, SLOT_F = 1, SLOT_SIGMA = 2, SLOT_ALPHA = 3, N_SLOTS = 4, SLOT
        N_FIELDS = N_SLOTS + WOST_MAX_SOURCES - 1 };
 struct alignas(16) DProgram {
     DField field[N_FIELDS];
-    float cheb_a[kChebA];
-    float cheb_b[kChebB];
     float sigma_bar;
     float sqrt_sigma_bar;
     float inv_sigma_bar;
@@ -399,29 +403,34 @@ WOST_HD float sigma_prime_from(const Jet& alpha, float sigma, bool detached) {
 // ---------------------------------------------------------------------------
 // Screened Green's function norm (solvers/utils.py:29-44):
 //   G_norm(R) = (1/sigma_bar) (1 - 1/I0(R sqrt(sigma_bar)))
-// with 1/I0(x) = exp(-x) / i0e(x); i0e from Chebyshev series whose
-// coefficients the host fits in double precision (wost_tables.cpp).
-// ---------------------------------------------------------------------------
-template <class CP>
-WOST_HD float cheb_eval(CP c, int n, float t) {
-    float b1 = 0.f, b2 = 0.f, t2 = 2.f * t;
-    for (int k = n - 1; k >= 1; --k) {
-        float b0 = t2 * b1 - b2 + c[k];
-        b2 = b1;
-        b1 = b0;
-    }
-    return t * b1 - b2 + c[0];
-}
+// With x = R sqrt(sigma_bar),
+//   G_norm(R) = R^2 Phi(x),  Phi(x) = (1 - 1/I0(x)) / x^2
+// Phi is smooth and slowly varying (1/4 at 0, 1/x^2 for large x), so a
+// piecewise cubic (Hermite data Phi, Phi' from the power series in double,
+// wost_tables.cpp greens_norm_cells) over kGnormCells cells of [0, kGnormXMax)
+// gives it to ~2 ulp in ~10 instructions and one LDS read (a Chebyshev i0e
+// + exp + reciprocal costs ~90). Beyond kGnormXMax,
+// 1 - 1/I0(x) rounds to 1.0f, so G_norm is 1/sigma_bar exactly, as in the
+// reference's float32 arithmetic. For small x the table is the exact value,
+// where the reference's float32 1 - 1/I0(x) loses digits to cancellation
+// (the difference is within that rounding).
+// Cell c holds the cubic's coefficients in t = x / h - c, h = 1/12 (exact
+// inverse, so t = fma(x, 12, -c) carries one rounding), cells up to 256/12.
+constexpr int kGnormCells = 256;
+constexpr float kGnormInvH = 12.0f;
+constexpr float kGnormXMax = (float)kGnormCells / kGnormInvH;
+constexpr int kSamplerFloatsPadded = (WOST_SAMPLER_TABLE_N + 3) & ~3;   // gnorm cells follow, 16-byte aligned
 
-template <class CP>
-WOST_HD float inv_i0(CP ca, CP cb, float x) {
-    float i0e;
-    if (x <= 8.0f) {
-        i0e = cheb_eval(ca, kChebA, x * 0.25f - 1.0f);
-    } else {
-        i0e = cheb_eval(cb, kChebB, 16.0f * f_rcp(x) - 1.0f) * f_rcp(f_sqrt(x));
-    }
-    return f_exp(-x) * f_rcp(i0e);
+template <class TabP>
+WOST_HD float greens_norm_from_table(TabP cells, float x, float r, float inv_sb) {
+#pragma clang fp contract(off)
+    const float xc = x < kGnormXMax ? x : kGnormXMax;
+    int c = (int)(xc * kGnormInvH);
+    c = c > kGnormCells - 1 ? kGnormCells - 1 : c;
+    const float t = fmaf(xc, kGnormInvH, -(float)c);
+    const float4 a = cells[c];
+    const float phi = fmaf(t, fmaf(t, fmaf(t, a.w, a.z), a.y), a.x);
+    return x < kGnormXMax ? (r * r) * phi : inv_sb;
 }
 
 // ---------------------------------------------------------------------------
@@ -452,8 +461,8 @@ WOST_HD float sample_rho(TabP tab, float u) {
 // distance_to_polyline_jit (:25-49): min over segments of the distance to the
 // clamped projection; a zero-length segment yields NaN which torch.min
 // propagates. sqrt is monotonic, so min(sqrt) == sqrt(min) bit for bit.
-template <class VP>
-WOST_HD float poly_distance(VP v, int nv, float px, float py) {
+template <class VP, class Div>
+WOST_HD float poly_distance_with(VP v, int nv, float px, float py, Div div) {
 #pragma clang fp contract(off)
     float best = WOST_INF;
     bool nan = false;
@@ -464,7 +473,7 @@ WOST_HD float poly_distance(VP v, int nv, float px, float py) {
         float vx = px - a.x, vy = py - a.y;
         float duv = vx * ux + vy * uy;
         float duu = ux * ux + uy * uy;
-        float t = duv / duu;
+        float t = div(i - 1, duv, duu);
         t = t < 0.f ? 0.f : t;   // torch.clamp keeps NaN
         t = t > 1.f ? 1.f : t;
         float cx = (1.0f - t) * a.x + t * b.x;
@@ -476,6 +485,36 @@ WOST_HD float poly_distance(VP v, int nv, float px, float py) {
         a = b;
     }
     return nan ? WOST_NAN : sqrtf(best);
+}
+
+template <class VP>
+WOST_HD float poly_distance(VP v, int nv, float px, float py) {
+    return poly_distance_with(v, nv, px, py, [](int, float duv, float duu) { return duv / duu; });
+}
+
+// The same with the projection's division by a segment's constant squared
+// length done as one Markstein step, q = duv y, duv - q duu (exact, fma),
+// q + r y, with y = RN(1/duu) given per segment (the specialised kernels
+// compile the polyline in, wost_jit.cpp). The generator passes y only for
+// lengths whose mantissa it has checked exhaustively (every duv mantissa gives
+// RN(duv/duu)) and 0 otherwise (plain division). Outside 2^-40 <= |q| <= 2^40,
+// where the check's scaling argument could meet underflow or overflow, the
+// lane's whole scan is redone with IEEE division.
+template <class VP>
+WOST_HD float poly_distance_rcp(VP v, const float* rcp, int nv, float px, float py) {
+    bool redo = false;
+    float d = poly_distance_with(v, nv, px, py, [&](int i, float duv, float duu) {
+        const float y = rcp[i];
+        if (y == 0.0f) return duv / duu;
+        const float q = duv * y;
+        const float aq = fabsf(q);
+        redo |= !(aq >= 0x1p-40f && aq <= 0x1p40f);
+        return fmaf(fmaf(-q, duu, duv), y, q);
+    });
+    if (WOST_ANY(redo)) {
+        if (redo) d = poly_distance(v, nv, px, py);
+    }
+    return d;
 }
 
 // is_silhouette_jit (:51-81) for interior vertex j in [1, nv-2].
@@ -549,6 +588,44 @@ WOST_HD float ray_segment_time_filtered(float2 a, float2 b, float qx, float qy, 
 
 struct Hit { float x, y, nx, ny; bool hit; int seg; };
 
+WOST_HD float bits_to_float(int32_t b) { return __builtin_bit_cast(float, b); }
+
+// Length dn = sqrtf(s2), s2 = dxi^2 + dyi^2, and the unit vector (dxi/dn,
+// dyi/dn) of a ray direction (PolylinesSimple.py:151-152), bit for bit the IEEE
+// operations. The walk's directions are (cos, sin), so s2 lies within 64 ulps
+// of 1, s2 = 1 + k 2^-23 (k >= 0) or 1 + k 2^-24 (k < 0), with k the
+// difference of the bit patterns of s2 and 1. There the correctly rounded
+//   sqrt(s2) = 1 + j 2^-23 (j = k>>1)        or 1 + j 2^-24 (j = -ceil(-k/2)),
+//   1/dn     = 1 - 2j 2^-24 (j >= 0)         or 1 + ceil(-j/2) 2^-23,
+// and a/dn is one Markstein step from y = RN(1/dn): q = RN(a y),
+// r = a - q dn (exact, fma), RN(q + r y) -- correctly rounded for every a with
+// 2^-100 <= |a| <= 2 and each of these 65 dn, checked exhaustively on the host
+// (tests/native/unit_dir_check.cpp). Anything else takes the IEEE operations.
+WOST_HD void unit_direction(float dxi, float dyi, float& dn, float& dx, float& dy) {
+#pragma clang fp contract(off)
+    const float s2 = dxi * dxi + dyi * dyi;
+    const int32_t k = __builtin_bit_cast(int32_t, s2) - 0x3F800000;
+#if defined(WOST_EXP_IEEE_DIRECTION)
+    const bool fast = false;
+#else
+    const bool fast = (uint32_t)(k + 64) <= 128u && fabsf(dxi) >= 0x1p-100f && fabsf(dyi) >= 0x1p-100f;
+#endif
+    const int32_t j = k >= 0 ? (k >> 1) : -((1 - k) >> 1);
+    const float n = bits_to_float(0x3F800000 + j);
+    const float y = bits_to_float(j >= 0 ? 0x3F800000 - 2 * j : 0x3F800000 + ((1 - j) >> 1));
+    const float qx = dxi * y, qy = dyi * y;
+    dn = n;
+    dx = fmaf(fmaf(-qx, n, dxi), y, qx);
+    dy = fmaf(fmaf(-qy, n, dyi), y, qy);
+    if (WOST_ANY(!fast)) {
+        if (!fast) {
+            dn = sqrtf(s2);
+            dx = dxi / dn;
+            dy = dyi / dn;
+        }
+    }
+}
+
 // Left unit normal of segment a->b (PolylinesSimple.py:189-194): (0, 1) for a
 // degenerate segment.
 WOST_HD float2 segment_left_normal(float2 sa, float2 sb) {
@@ -590,12 +667,12 @@ template <bool NORMAL = true, class VP>
 WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
     Hit h;
-    float dn = sqrtf(dxi * dxi + dyi * dyi);
+    float dn, dx, dy;
+    unit_direction(dxi, dyi, dn, dx, dy);
     if (dn < 1e-10f) {
         h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
         return h;
     }
-    float dx = dxi / dn, dy = dyi / dn;
     float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
     float best = WOST_INF;
     int bi = -1;
@@ -764,12 +841,12 @@ template <bool NORMAL = true>
 WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
     Hit h;
-    float dn = sqrtf(dxi * dxi + dyi * dyi);
+    float dn, dx, dy;
+    unit_direction(dxi, dyi, dn, dx, dy);
     if (dn < 1e-10f) {
         h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
         return h;
     }
-    const float dx = dxi / dn, dy = dyi / dn;
     const float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
     const float tol = t.tol + 6.103515625e-05f * (fabsf(qx) + fabsf(qy));   // + 2^-14 |q|_1
     const int nseg = t.nv - 1;

@@ -32,7 +32,11 @@ inline bool mode_src(int m) {
 inline bool mode_delta(int m) { return m == MODE_DELTA || m == MODE_MIXED_DELTA || m == MODE_MIXED_DELTA_TREE; }
 
 inline size_t walk_lds_bytes(int mode, int nd, int nn, int n_points) {
-    return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points, mode_tree(mode));
+    return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points, mode_tree(mode), mode_delta(mode));
+}
+// floats of the sampler / G_norm table buffer (WalkArgs::table)
+inline size_t table_floats(bool delta) {
+    return (size_t)kSamplerFloatsPadded + (delta ? 4 * (size_t)kGnormCells : 0);
 }
 
 // precompiled (interpreted-field) walk kernels

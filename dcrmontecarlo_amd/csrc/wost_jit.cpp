@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -25,6 +26,63 @@ namespace wost {
 namespace {
 
 // Exact float32 literal (hex float), or a builtin for non-finite values.
+// y = RN(1/duu) for the segment a->b when the Markstein step q + (duv - q duu) y
+// (q = RN(duv y)) equals RN(duv / duu) for every duv mantissa (checked
+// exhaustively, once per mantissa of duu, cached), else 0 (wost_device.h
+// poly_distance_rcp). duu is formed exactly like the kernel forms it.
+// A/B switches for tools/ab_bench.sh (WOST_EXP_FLAGS, a bit mask; 0 in
+// production): 1 plain division in poly_distance, 2 IEEE unit_direction.
+// Each bit only selects one fixed code path.
+int exp_flags() {
+    const char* e = std::getenv("WOST_EXP_FLAGS");
+    return e ? (int)std::strtol(e, nullptr, 10) & 3 : 0;
+}
+
+float markstein_reciprocal(float ax, float ay, float bx, float by) {
+#pragma clang fp contract(off)
+    volatile float ux = bx - ax, uy = by - ay;
+    volatile float duu = ux * ux + uy * uy;
+    const float d = duu;
+    if (!(d >= 0x1p-40f && d <= 0x1p40f)) return 0.0f;
+    uint32_t db;
+    std::memcpy(&db, &d, 4);
+    const uint32_t mant = db & 0x7FFFFFu;
+    if (mant == 0) return 0.0f;   // a power of two: the compiler folds the division into an exact multiply
+    if (exp_flags() & 1) return 0.0f;   // A/B switch: plain division
+    static std::mutex mu;
+    static std::map<uint32_t, bool> ok_cache;
+    bool ok;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = ok_cache.find(mant);
+        if (it != ok_cache.end()) {
+            ok = it->second;
+        } else {
+            if (ok_cache.size() >= 64) return 0.0f;   // bound the host time (~25 ms per length)
+            const uint32_t bb = 0x3F800000u | mant;
+            float b;
+            std::memcpy(&b, &bb, 4);
+            volatile float one = 1.0f, vb = b;
+            const float y = one / vb;
+            ok = true;
+            for (uint32_t m = 0; m < (1u << 23) && ok; ++m) {
+                const uint32_t ab = 0x3F800000u | m;
+                float a;
+                std::memcpy(&a, &ab, 4);
+                const float q = a * y;
+                const float got = std::fma(std::fma(-q, b, a), y, q);
+                volatile float va = a;
+                const float want = va / vb;
+                ok = std::memcmp(&got, &want, 4) == 0;
+            }
+            ok_cache[mant] = ok;
+        }
+    }
+    if (!ok) return 0.0f;
+    volatile float one = 1.0f;
+    return one / d;
+}
+
 std::string lit(float v) {
     if (v != v) return "__builtin_nanf(\"\")";
     if (v == __builtin_inff()) return "__builtin_inff()";
@@ -202,6 +260,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     const DField& fS = hdr.field[SLOT_SIGMA];
     const DField& fA = hdr.field[SLOT_ALPHA];
     std::ostringstream o;
+    if (exp_flags() & 2) o << "#define WOST_EXP_IEEE_DIRECTION 1\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
@@ -230,18 +289,26 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    __device__ __forceinline__ float sigma_bar() const { return " << lit(hdr.sigma_bar) << "; }\n";
     o << "    __device__ __forceinline__ float sqrt_sigma_bar() const { return " << lit(hdr.sqrt_sigma_bar) << "; }\n";
     o << "    __device__ __forceinline__ float inv_sigma_bar() const { return " << lit(hdr.inv_sigma_bar) << "; }\n";
-    o << "    __device__ __forceinline__ float inv_i0(float x) const {\n        const float ca[" << kChebA << "] = {";
-    for (int k = 0; k < kChebA; ++k) o << (k ? ", " : "") << lit(hdr.cheb_a[k]);
-    o << "};\n        const float cb[" << kChebB << "] = {";
-    for (int k = 0; k < kChebB; ++k) o << (k ? ", " : "") << lit(hdr.cheb_b[k]);
-    o << "};\n        return wost::inv_i0(ca, cb, x);\n    }\n";
     // a short Dirichlet polyline is compiled in: the scan unrolls, the segment
     // vectors and squared lengths fold to constants (the same IEEE operations)
     o << "    __device__ __forceinline__ float dirichlet_distance(const float2* sD, int nd, float x, float y) const {\n";
     if (nd <= kJitMaxConstVertices) {
         o << "        const float2 v[" << nd << "] = {";
         for (int i = 0; i < nd; ++i) o << (i ? ", " : "") << "{" << lit(dverts[2 * i]) << ", " << lit(dverts[2 * i + 1]) << "}";
-        o << "};\n        return wost::poly_distance(v, " << nd << ", x, y);\n";
+        o << "};\n";
+        // reciprocal squared segment lengths for the Markstein division (0: divide)
+        bool any = false;
+        std::ostringstream r;
+        for (int i = 0; i + 1 < nd; ++i) {
+            const float y = markstein_reciprocal(dverts[2 * i], dverts[2 * i + 1], dverts[2 * i + 2], dverts[2 * i + 3]);
+            any |= y != 0.0f;
+            r << (i ? ", " : "") << lit(y);
+        }
+        if (any && nd >= 2)
+            o << "        const float rcp[" << nd - 1 << "] = {" << r.str() << "};\n"
+              << "        return wost::poly_distance_rcp(v, rcp, " << nd << ", x, y);\n";
+        else
+            o << "        return wost::poly_distance(v, " << nd << ", x, y);\n";
     } else {
         o << "        return wost::poly_distance(sD, nd, x, y);\n";
     }

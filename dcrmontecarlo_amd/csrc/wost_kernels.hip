@@ -83,7 +83,6 @@ struct InterpFields {
     DField fG, fF, fS, fA;
     bool det;
     float sb, sqsb, isb;
-    FloatsC ca, cb;
     __device__ __forceinline__ explicit InterpFields(const char* prog) : P(prog) {
         fG = P.field(SLOT_G);
         fF = P.field(SLOT_F);
@@ -93,8 +92,6 @@ struct InterpFields {
         sb = P.hdr->sigma_bar;
         sqsb = P.hdr->sqrt_sigma_bar;
         isb = P.hdr->inv_sigma_bar;
-        ca.p = (cptr<float>)P.hdr->cheb_a;
-        cb.p = (cptr<float>)P.hdr->cheb_b;
     }
     __device__ __forceinline__ bool has_g() const { return fG.present != 0; }
     __device__ __forceinline__ float g(float x, float y) const { return P.value(fG, x, y); }
@@ -106,7 +103,6 @@ struct InterpFields {
     __device__ __forceinline__ float sigma_bar() const { return sb; }
     __device__ __forceinline__ float sqrt_sigma_bar() const { return sqsb; }
     __device__ __forceinline__ float inv_sigma_bar() const { return isb; }
-    __device__ __forceinline__ float inv_i0(float x) const { return wost::inv_i0(ca, cb, x); }
     __device__ __forceinline__ float dirichlet_distance(const float2* sD, int nd, float x, float y) const {
         return poly_distance(sD, nd, x, y);
     }

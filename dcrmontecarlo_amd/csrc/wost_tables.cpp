@@ -91,6 +91,46 @@ double screened_greens(double r, double R, double sigma_bar) {
     return (k0_host(r * s) - (kR / iR) * i0_host(r * s)) / (2.0 * kPi);
 }
 
+void greens_phi(double x, double* phi, double* dphi) {
+    // q = x^2/4; I0 = sum q^k/(k!)^2; A = (I0 - 1)/q = sum_{k>=1} q^(k-1)/(k!)^2;
+    // Phi = A / (4 I0). dA/dx = (x/2) sum_{k>=2} (k-1) q^(k-2)/(k!)^2; I1 = (x/2) sum q^k/(k!(k+1)!)
+    const double q = 0.25 * x * x;
+    double i0 = 1.0, A = 0.0, dAq = 0.0, s1 = 0.0;
+    double t = 1.0;        // q^k / (k!)^2
+    double tq = 1.0;       // q^(k-1) / (k!)^2 (k >= 1)
+    double tqq = 0.0;      // q^(k-2) / (k!)^2 (k >= 2)
+    s1 = 1.0;              // k = 0 term of sum q^k/(k!(k+1)!)
+    for (int k = 1; k < 200; ++k) {
+        const double kk = (double)k * k;
+        t = t * q / kk;
+        tq = (k == 1) ? 1.0 : tq * q / kk;
+        tqq = (k == 2) ? 0.25 : (k > 2 ? tqq * q / kk : 0.0);
+        i0 += t;
+        A += tq;
+        dAq += (k - 1) * tqq;
+        s1 += t / (k + 1);
+        if (t < 1e-18 * i0 && k > 4) break;
+    }
+    const double i1 = 0.5 * x * s1;
+    const double dA = 0.5 * x * dAq;
+    *phi = A / (4.0 * i0);
+    *dphi = (dA * i0 - A * i1) / (4.0 * i0 * i0);
+}
+
+void greens_norm_cells(float* out, int cells, double xmax) {
+    const double h = xmax / cells;
+    for (int c = 0; c < cells; ++c) {
+        double p0, d0, p1, d1;
+        greens_phi(c * h, &p0, &d0);
+        greens_phi((c + 1) * h, &p1, &d1);
+        const double m0 = h * d0, m1 = h * d1;
+        out[4 * c + 0] = (float)p0;
+        out[4 * c + 1] = (float)m0;
+        out[4 * c + 2] = (float)(3.0 * (p1 - p0) - 2.0 * m0 - m1);
+        out[4 * c + 3] = (float)(2.0 * (p0 - p1) + m0 + m1);
+    }
+}
+
 void greens_sampler_nodes(float* out, int n) {
     const double a = 1e-6;
     const double c0 = a - a * std::log(a);

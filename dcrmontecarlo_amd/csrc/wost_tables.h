@@ -24,6 +24,15 @@ double screened_greens_norm(double R, double sigma_bar);
 // screenedGreens2D at distance r for ball radius R (solvers/utils.py:5-26), double.
 double screened_greens(double r, double R, double sigma_bar);
 
+// Cubic coefficients {a0, a1, a2, a3} per cell (4 floats each) of
+// Phi(x) = (1 - 1/I0(x)) / x^2 on cells [c h, (c+1) h), h = xmax / cells,
+// in t = x/h - c: Hermite interpolation of Phi and h Phi' at the cell ends,
+// both from the power series of I0 and I1 in double (wost_device.h
+// greens_norm_from_table).
+void greens_norm_cells(float* out, int cells, double xmax);
+// Phi(x) and Phi'(x) in double.
+void greens_phi(double x, double* phi, double* dphi);
+
 // Inverse-CDF nodes F^-1(i/(n-1)), i = 0..n-1, of
 //  * GreensDistribution2D (solvers/utils.py:138-151): density -log(rho) on [1e-6, 1);
 //  * ScreenedGreensDistribution2D (solvers/utils.py:181-195): density

@@ -66,17 +66,19 @@ WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
 // Bytes of dynamic LDS a walk-kernel workgroup needs. With the segment tree
 // the Neumann polyline stays in global memory (read through the caches).
-WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false) {
+WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false,
+                                  bool delta = false) {
     size_t b = align16(sizeof(float2) * (size_t)nd);
     if (neu && !tree) b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
-    if (src) b += align16(sizeof(float) * WOST_SAMPLER_TABLE_N);
+    if (src) b += sizeof(float) * (size_t)kSamplerFloatsPadded;
+    if (delta) b += sizeof(float4) * (size_t)kGnormCells;
     if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
     return b;
 }
 
 // The Fields policy F provides: has_g(), g(x,y), f(x,y), sigma(x,y),
 // alpha(x,y), alpha_jet(x,y), detached(), sigma_bar(), sqrt_sigma_bar(),
-// inv_sigma_bar(), inv_i0(x), and the polyline scans dirichlet_distance(sD,
+// inv_sigma_bar(), and the polyline scans dirichlet_distance(sD,
 // nd, x, y), neumann_silhouette_distance(sN, nn, x, y), neumann_intersect(sN,
 // nn, x, y, dx, dy, r) (the interpreted kernels scan the staged vertices; the
 // specialised ones may have them compiled in). TREE: Neumann queries through
@@ -98,8 +100,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                                            ((NEU && !TREE) ? align16(sizeof(float2) * (size_t)A.nn) : 0));
     float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sPhi) +
                                          ((NEU && !TREE) ? align16(sizeof(float) * (size_t)(A.nn > 1 ? A.nn - 1 : 0)) : 0));
-    float2* sP = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(sT) +
-                                           (SRC ? align16(sizeof(float) * WOST_SAMPLER_TABLE_N) : 0));
+    float4* sG = reinterpret_cast<float4*>(sT + (SRC ? kSamplerFloatsPadded : 0));   // G_norm cells
+    float2* sP = reinterpret_cast<float2*>(sG + (DELTA ? kGnormCells : 0));
     const bool points_in_lds = A.n_points <= kLdsPointsMax;
 
     for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
@@ -110,6 +112,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_leaf, A.tree_tol};
     if (SRC)
         for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
+    if (DELTA) {
+        const float4* g = reinterpret_cast<const float4*>(A.table + kSamplerFloatsPadded);
+        for (int i = threadIdx.x; i < kGnormCells; i += blockDim.x) sG[i] = g[i];
+    }
     if (points_in_lds)
         for (int i = threadIdx.x; i < A.n_points; i += blockDim.x) sP[i] = A.points[i];
     __syncthreads();
@@ -254,7 +260,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             if (a2 > b2) clipped = sqrtf(a2) > sqrtf(b2);
             if (clipped) { yx = xnx; yy = xny; }
             if (DELTA) {
-                gnorm = inv_sb * (1.0f - fld.inv_i0(r * sqrt_sb));   // solvers/utils.py:43-44
+                gnorm = greens_norm_from_table(sG, r * sqrt_sb, r, inv_sb);   // solvers/utils.py:29-44
                 aj = fld.alpha_jet(yx, yy);
             }
             if constexpr (NS == 1) {

@@ -49,6 +49,26 @@ def point_sums(block_stats: np.ndarray, n_points: int) -> np.ndarray:
     return acc
 
 
+def replicate_points(points: np.ndarray, world: int) -> np.ndarray:
+    """Weak scaling: the survey's points once per rank, [world * N, 2]. Copy r is
+    points r*N .. r*N+N-1, so its walk ids (point * nWalks + walk) are distinct
+    from every other copy's and, with the blocks sharded by shard_range, rank r
+    solves exactly copy r: the one-GPU workload, on its own random streams."""
+    p = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 2))
+    return np.ascontiguousarray(np.tile(p, (world, 1)))
+
+
+def merge_replicas(sums: np.ndarray, world: int) -> np.ndarray:
+    """Per-point (sum, sum^2, steps) of replicate_points' copies merged in rank
+    order: [world * N, 3] -> [N, 3], the statistics of world * nWalks walks per point."""
+    n = sums.shape[0] // world
+    b = sums.reshape(world, n, sums.shape[1])
+    acc = np.zeros((n, sums.shape[1]), np.float64)
+    for r in range(world):
+        acc += b[r]
+    return acc
+
+
 def solve_distributed(solver, points, nWalks: int, maxSteps: int = 1000, eps: float = 1e-4, seed: int = 0,
                       group=None, device=None):
     """WostSolver_2D.solve across the ranks of ``group`` (torch.distributed must be

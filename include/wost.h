@@ -283,6 +283,12 @@ int wost_eval_field(wost_handle* h, int32_t which, const float* points, int64_t 
 /* The radial sampler's inverse-CDF nodes (WOST_SAMPLER_TABLE_N floats). */
 int wost_sampler_table(const wost_handle* h, float* out, int32_t n);
 
+/* The walk kernels' screened Green's norm G_norm(R) for this sigma_bar
+ * (replaces screenedGreensNorm2D, solvers/utils.py:29-44, at
+ * solvers/WoStSolver.py:250), evaluated on the host with the kernels' own
+ * table and arithmetic: out[i] = G_norm(radii[i]). No device needed. */
+int wost_greens_norm(double sigma_bar, const float* radii, int64_t n, float* out);
+
 /* Batched polyline queries on the device (geometry/PolylinesSimple.py).
  *   op 0 distance          (:25-49, :214-224)   out_f[n]
  *   op 1 isSilhouette      (:51-81, :242-253)   out_mask[n][nv-2]

@@ -57,6 +57,20 @@ def test_gloo_gather_matches_single_rank(world):
         assert np.array_equal(res[r], single)
 
 
+def test_replicas_shard_one_copy_per_rank_and_merge():
+    pts = np.arange(10, dtype=np.float32).reshape(5, 2)
+    for world in (1, 2, 3, 8):
+        rep = D.replicate_points(pts, world)
+        assert rep.shape == (5 * world, 2) and np.array_equal(rep[5 * (world - 1):], pts)
+        for nbpp in (1, 3, 245):
+            nb = rep.shape[0] * nbpp
+            for r in range(world):   # rank r's blocks are exactly copy r's
+                assert D.shard_range(nb, r, world) == (r * 5 * nbpp, (r + 1) * 5 * nbpp)
+        rows = np.stack([np.arange(5 * world, dtype=np.float64)] * 3, axis=1)
+        m = D.merge_replicas(rows, world)
+        assert np.array_equal(m[:, 0], sum(np.arange(5) + 5 * r for r in range(world)))
+
+
 def test_shard_ranges_partition_blocks():
     for nb in (1, 7, 48 * 245):
         for world in (1, 2, 3, 8):
