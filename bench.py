@@ -74,6 +74,13 @@ def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
     base = {"value": float(s.sum()) / dt, "unit": "walk-steps/s", "cores": threads, "kind": "port",
             "sample": f"dcr_dipole {len(pts)} electrodes x {w} walks ({int(s.sum())} walk-steps, {dt:.1f} s), "
                       f"oracle/wost_oracle.c with {threads} OpenMP threads"}
+    # the same oracle on one core, on a smaller sample (all cores and one core)
+    w1 = max(16, int(w * threads * 0.25 / 16))
+    t0 = time.perf_counter()
+    _, s1 = pb.solve_walks(pts, w1, sc.max_steps, sc.eps, CPU_SEED + 1, threads=1)
+    dt1 = time.perf_counter() - t0
+    base["single_core"] = {"value": float(s1.sum()) / dt1, "cores": 1,
+                           "sample": f"{len(pts)} electrodes x {w1} walks ({int(s1.sum())} walk-steps, {dt1:.1f} s)"}
     vh, _ = O.Problem.from_scenario(sc_h, sigma_bar=sigma_bar_h).solve_walks(pts, w, sc.max_steps, sc.eps, CPU_SEED,
                                                                              threads=threads)
     return base, w, _point_stats(v, w), _point_stats(vh, w)
@@ -104,7 +111,10 @@ def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu):
             "walks_per_electrode": int(w_cpu), "seed": CPU_SEED, "resolved": cmp["resolved"],
             "rmse": cmp["rmse"], "cpu_mc_1sigma_rms": cmp["mc_1sigma"],
             "rmse_over_1sigma": (cmp["rmse"] / cmp["mc_1sigma"]) if cmp["rmse"] is not None and cmp["mc_1sigma"] else None,
-            "gpu_full_rmse": cmp_full["rmse"]}
+            "z_rms_same_walks": cmp["z_rms"],
+            "gpu_full_rmse": cmp_full["rmse"],
+            # the full run's walks are independent of the sample's: z-scores of the two estimates
+            "gpu_full_vs_cpu_z_rms": cmp_full["z_rms"], "gpu_full_vs_cpu_z_max": cmp_full["z_max"]}
     return out
 
 

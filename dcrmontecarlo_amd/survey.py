@@ -121,14 +121,18 @@ def run_dipole_dipole(sc: Scenario, alpha_bg: float, n_walks: int, seed: int = 0
 
 
 def compare(a: ApparentResistivity, b: ApparentResistivity) -> dict:
-    """RMSE of rho_a between two solutions over dipoles resolved in both, and the
-    RMS of b's Monte-Carlo 1-sigma over the same dipoles (the north-star bound)."""
+    """RMSE of rho_a between two solutions over dipoles resolved in both, the RMS
+    of b's Monte-Carlo 1-sigma over the same dipoles (the north-star bound), and
+    the z-scores z_i = (a_i - b_i) / sqrt(se_a^2 + se_b^2) (RMS z <= 1.2,
+    max |z| < 4 for independent solutions)."""
     ok = a.resolved & b.resolved & np.isfinite(a.rho_a) & np.isfinite(b.rho_a)
     if not ok.any():
-        return {"rmse": None, "mc_1sigma": None, "resolved": 0}
+        return {"rmse": None, "mc_1sigma": None, "resolved": 0, "z_rms": None, "z_max": None}
     d = a.rho_a[ok] - b.rho_a[ok]
+    s = np.sqrt(a.se[ok] ** 2 + b.se[ok] ** 2)
+    z = np.where(s > 0, d / np.where(s > 0, s, 1.0), 0.0)
     return {"rmse": float(np.sqrt(np.mean(d * d))), "mc_1sigma": float(np.sqrt(np.mean(b.se[ok] ** 2))),
-            "resolved": int(ok.sum())}
+            "resolved": int(ok.sum()), "z_rms": float(np.sqrt(np.mean(z * z))), "z_max": float(np.max(np.abs(z)))}
 
 
 @dataclass

@@ -56,7 +56,9 @@ def test_compare_uses_jointly_resolved_dipoles():
     assert c["rmse"] == pytest.approx(0.1)
     assert c["mc_1sigma"] == pytest.approx(0.2)
     none = survey.compare(a, survey.ApparentResistivity(b.rho_a, b.se, np.zeros(3, bool)))
-    assert none == {"rmse": None, "mc_1sigma": None, "resolved": 0}
+    assert none == {"rmse": None, "mc_1sigma": None, "resolved": 0, "z_rms": None, "z_max": None}
+    assert c["z_max"] == pytest.approx(0.1 / np.sqrt(0.05))
+    assert c["z_rms"] == pytest.approx(0.1 / np.sqrt(0.05))
 
 
 def test_homogeneous_scenario_keeps_survey():
