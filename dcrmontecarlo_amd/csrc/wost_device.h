@@ -172,6 +172,13 @@ WOST_HD float fv_exp_quad(float x, float y, float cx, float cy, float axx, float
     float dx = x - cx, dy = y - cy;
     return f_exp(axx * (dx * dx) + ayy * (dy * dy) + axy * (dx * dy) + ax * dx + ay * dy + a0);
 }
+// The axis-aligned Gaussian (axy = ax = ay = a0 = 0, the usual current source):
+// the dropped terms only add signed zeros, so the value is fv_exp_quad's.
+WOST_HD float fv_exp_quad_diag(float x, float y, float cx, float cy, float axx, float ayy) {
+    float dx = x - cx, dy = y - cy;
+    return f_exp(axx * (dx * dx) + ayy * (dy * dy));
+}
+WOST_HD bool exp_quad_is_diag(const float* p) { return p[4] == 0.f && p[5] == 0.f && p[6] == 0.f && p[7] == 0.f; }
 WOST_HD float fv_sin_lin(float x, float y, float a, float b, float c) { return f_sin(a * x + b * y + c); }
 WOST_HD float fv_cos_lin(float x, float y, float a, float b, float c) { return f_cos(a * x + b * y + c); }
 WOST_HD float fv_sigmoid_lin(float x, float y, float a, float b, float c) { return sigmoidf(a * x + b * y + c); }
@@ -209,6 +216,13 @@ WOST_HD Jet fj_exp_quad(float x, float y, float cx, float cy, float axx, float a
     float e = f_exp(axx * (dx * dx) + ayy * (dy * dy) + axy * (dx * dy) + ax * dx + ay * dy + a0);
     float qx = 2.f * axx * dx + axy * dy + ax;
     float qy = 2.f * ayy * dy + axy * dx + ay;
+    return Jet{e, e * qx, e * qy, e * (qx * qx + qy * qy + 2.f * (axx + ayy))};
+}
+WOST_HD Jet fj_exp_quad_diag(float x, float y, float cx, float cy, float axx, float ayy) {
+    float dx = x - cx, dy = y - cy;
+    float e = f_exp(axx * (dx * dx) + ayy * (dy * dy));
+    float qx = 2.f * axx * dx;
+    float qy = 2.f * ayy * dy;
     return Jet{e, e * qx, e * qy, e * (qx * qx + qy * qy + 2.f * (axx + ayy))};
 }
 WOST_HD Jet fj_sin_lin(float x, float y, float a, float b, float c) {
@@ -315,7 +329,9 @@ WOST_HD float factor_value(const DFactor& f, float x, float y, const float* grid
     const float* p = f.p;
     switch (f.kind) {
     case WOST_FK_MONO: return fv_mono(x, y, (int)p[0], (int)p[1]);
-    case WOST_FK_EXP_QUAD: return fv_exp_quad(x, y, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
+    case WOST_FK_EXP_QUAD:
+        return exp_quad_is_diag(p) ? fv_exp_quad_diag(x, y, p[0], p[1], p[2], p[3])
+                                   : fv_exp_quad(x, y, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
     case WOST_FK_SIN_LIN: return fv_sin_lin(x, y, p[0], p[1], p[2]);
     case WOST_FK_COS_LIN: return fv_cos_lin(x, y, p[0], p[1], p[2]);
     case WOST_FK_SIGMOID_LIN: return fv_sigmoid_lin(x, y, p[0], p[1], p[2]);
@@ -331,7 +347,9 @@ WOST_HD Jet factor_jet(const DFactor& f, float x, float y, const float* grid) {
     const float* p = f.p;
     switch (f.kind) {
     case WOST_FK_MONO: return fj_mono(x, y, (int)p[0], (int)p[1]);
-    case WOST_FK_EXP_QUAD: return fj_exp_quad(x, y, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
+    case WOST_FK_EXP_QUAD:
+        return exp_quad_is_diag(p) ? fj_exp_quad_diag(x, y, p[0], p[1], p[2], p[3])
+                                   : fj_exp_quad(x, y, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7]);
     case WOST_FK_SIN_LIN: return fj_sin_lin(x, y, p[0], p[1], p[2]);
     case WOST_FK_COS_LIN: return fj_cos_lin(x, y, p[0], p[1], p[2]);
     case WOST_FK_SIGMOID_LIN: return fj_sigmoid_lin(x, y, p[0], p[1], p[2]);
@@ -492,25 +510,52 @@ WOST_HD float poly_distance(VP v, int nv, float px, float py) {
     return poly_distance_with(v, nv, px, py, [](int, float duv, float duu) { return duv / duu; });
 }
 
-// The same with the projection's division by a segment's constant squared
-// length done as one Markstein step, q = duv y, duv - q duu (exact, fma),
-// q + r y, with y = RN(1/duu) given per segment (the specialised kernels
-// compile the polyline in, wost_jit.cpp). The generator passes y only for
-// lengths whose mantissa it has checked exhaustively (every duv mantissa gives
-// RN(duv/duu)) and 0 otherwise (plain division). Outside 2^-40 <= |q| <= 2^40,
-// where the check's scaling argument could meet underflow or overflow, the
-// lane's whole scan is redone with IEEE division.
+// poly_distance for a polyline compiled into the kernel (wost_jit.cpp) whose
+// segments all have 0 < duu and coordinates below 2^60, at a point with
+// |px|, |py| <= 2^60: every quantity is then finite, so
+//  * no NaN can arise (the NaN bookkeeping goes) and the clamps and the min
+//    are fmaxf / fminf;
+//  * an axis-parallel segment's zero term vy * 0 (or vx * 0) only adds a
+//    signed zero, and the sign of a zero t never reaches d2 (t = +-0 gives
+//    1 - t = 1 and a zero t * b that cannot change a nonzero sum; a zero
+//    coordinate difference is squared);
+//  * the division by the constant duu is one Markstein step, q = duv y,
+//    r = duv - q duu (exact, fma), q + r y, with y = RN(1/duu) given per
+//    segment; the generator passes y only for lengths whose mantissa it has
+//    checked exhaustively (every duv mantissa gives RN(duv/duu)), else 0
+//    (plain division). Outside 2^-40 <= |q| <= 2^40, where the check's scaling
+//    argument could meet underflow, the lane redoes the scan with poly_distance.
+// The result is bit for bit poly_distance's.
 template <class VP>
-WOST_HD float poly_distance_rcp(VP v, const float* rcp, int nv, float px, float py) {
-    bool redo = false;
-    float d = poly_distance_with(v, nv, px, py, [&](int i, float duv, float duu) {
-        const float y = rcp[i];
-        if (y == 0.0f) return duv / duu;
-        const float q = duv * y;
-        const float aq = fabsf(q);
-        redo |= !(aq >= 0x1p-40f && aq <= 0x1p40f);
-        return fmaf(fmaf(-q, duu, duv), y, q);
-    });
+WOST_HD float poly_distance_const(VP v, const float* rcp, int nv, float px, float py) {
+#pragma clang fp contract(off)
+    bool redo = !(fabsf(px) <= 0x1p60f && fabsf(py) <= 0x1p60f);
+    float best = WOST_INF;
+    float2 a = v[0];
+    for (int i = 1; i < nv; ++i) {
+        const float2 b = v[i];
+        const float ux = b.x - a.x, uy = b.y - a.y;
+        const float vx = px - a.x, vy = py - a.y;
+        const float duv = uy == 0.0f ? vx * ux : (ux == 0.0f ? vy * uy : vx * ux + vy * uy);
+        const float duu = ux * ux + uy * uy;
+        const float y = rcp[i - 1];
+        float t;
+        if (y == 0.0f) {
+            t = duv / duu;
+        } else {
+            const float q = duv * y;
+            const float aq = fabsf(q);
+            redo |= !(aq >= 0x1p-40f && aq <= 0x1p40f);
+            t = fmaf(fmaf(-q, duu, duv), y, q);
+        }
+        t = fminf(fmaxf(t, 0.0f), 1.0f);
+        const float cx = (1.0f - t) * a.x + t * b.x;
+        const float cy = (1.0f - t) * a.y + t * b.y;
+        const float ex = cx - px, ey = cy - py;
+        best = fminf(best, ex * ex + ey * ey);
+        a = b;
+    }
+    float d = sqrtf(best);
     if (WOST_ANY(redo)) {
         if (redo) d = poly_distance(v, nv, px, py);
     }

@@ -31,24 +31,29 @@ namespace {
 // exhaustively, once per mantissa of duu, cached), else 0 (wost_device.h
 // poly_distance_rcp). duu is formed exactly like the kernel forms it.
 // A/B switches for tools/ab_bench.sh (WOST_EXP_FLAGS, a bit mask; 0 in
-// production): 1 plain division in poly_distance, 2 IEEE unit_direction.
+// production): 1 generic poly_distance for compiled-in polylines, 2 IEEE
+// unit_direction.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
     return e ? (int)std::strtol(e, nullptr, 10) & 3 : 0;
 }
 
-float markstein_reciprocal(float ax, float ay, float bx, float by) {
+// the squared segment length exactly as the kernel forms it
+float segment_duu(float ax, float ay, float bx, float by) {
 #pragma clang fp contract(off)
     volatile float ux = bx - ax, uy = by - ay;
     volatile float duu = ux * ux + uy * uy;
-    const float d = duu;
+    return duu;
+}
+
+float markstein_reciprocal(float ax, float ay, float bx, float by) {
+    const float d = segment_duu(ax, ay, bx, by);
     if (!(d >= 0x1p-40f && d <= 0x1p40f)) return 0.0f;
     uint32_t db;
     std::memcpy(&db, &d, 4);
     const uint32_t mant = db & 0x7FFFFFu;
     if (mant == 0) return 0.0f;   // a power of two: the compiler folds the division into an exact multiply
-    if (exp_flags() & 1) return 0.0f;   // A/B switch: plain division
     static std::mutex mu;
     static std::map<uint32_t, bool> ok_cache;
     bool ok;
@@ -100,11 +105,13 @@ std::string factor_call(const DFactor& f, bool jet) {
     case WOST_FK_MONO:
         o << pre << "mono(x, y, " << (int)p[0] << ", " << (int)p[1] << ")";
         break;
-    case WOST_FK_EXP_QUAD:
-        o << pre << "exp_quad(x, y";
-        for (int k = 0; k < 8; ++k) o << ", " << lit(p[k]);
+    case WOST_FK_EXP_QUAD: {
+        const bool diag = exp_quad_is_diag(p);   // the interpreter makes the same choice
+        o << pre << (diag ? "exp_quad_diag(x, y" : "exp_quad(x, y");
+        for (int k = 0; k < (diag ? 4 : 8); ++k) o << ", " << lit(p[k]);
         o << ")";
         break;
+    }
     case WOST_FK_SIN_LIN:
         o << pre << "sin_lin(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ")";
         break;
@@ -296,17 +303,19 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "        const float2 v[" << nd << "] = {";
         for (int i = 0; i < nd; ++i) o << (i ? ", " : "") << "{" << lit(dverts[2 * i]) << ", " << lit(dverts[2 * i + 1]) << "}";
         o << "};\n";
-        // reciprocal squared segment lengths for the Markstein division (0: divide)
-        bool any = false;
+        // poly_distance_const when every segment has 0 < duu and the coordinates are
+        // below 2^60, with the reciprocal squared lengths for the Markstein division
+        bool ok = nd >= 2 && !(exp_flags() & 1);
         std::ostringstream r;
-        for (int i = 0; i + 1 < nd; ++i) {
-            const float y = markstein_reciprocal(dverts[2 * i], dverts[2 * i + 1], dverts[2 * i + 2], dverts[2 * i + 3]);
-            any |= y != 0.0f;
-            r << (i ? ", " : "") << lit(y);
+        for (int i = 0; i < nd && ok; ++i) ok = std::fabs(dverts[2 * i]) <= 0x1p60f && std::fabs(dverts[2 * i + 1]) <= 0x1p60f;
+        for (int i = 0; ok && i + 1 < nd; ++i) {
+            ok = segment_duu(dverts[2 * i], dverts[2 * i + 1], dverts[2 * i + 2], dverts[2 * i + 3]) > 0.0f;
+            r << (i ? ", " : "")
+              << lit(markstein_reciprocal(dverts[2 * i], dverts[2 * i + 1], dverts[2 * i + 2], dverts[2 * i + 3]));
         }
-        if (any && nd >= 2)
+        if (ok)
             o << "        const float rcp[" << nd - 1 << "] = {" << r.str() << "};\n"
-              << "        return wost::poly_distance_rcp(v, rcp, " << nd << ", x, y);\n";
+              << "        return wost::poly_distance_const(v, rcp, " << nd << ", x, y);\n";
         else
             o << "        return wost::poly_distance(v, " << nd << ", x, y);\n";
     } else {
