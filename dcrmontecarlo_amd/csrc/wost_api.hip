@@ -276,6 +276,8 @@ int ensure_table(wost_handle* h) {
     if (h->delta) {
         screened_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N, h->sigma_bar);
         greens_norm_cells(h->table.data() + kSamplerFloatsPadded, kGnormCells, (double)kGnormCells / kGnormInvH);
+    } else if (h->compat == WOST_COMPAT_FIXED) {
+        greens_sampler_nodes_jacobian(h->table.data(), WOST_SAMPLER_TABLE_N);
     } else {
         greens_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N);
     }
@@ -331,6 +333,8 @@ bool use_tree(const wost_handle* h) {
 int walk_mode(const wost_handle* h) {
     const bool neu = !h->nverts.empty();
     const bool src = h->fields[SLOT_F].present;
+    if (h->compat == WOST_COMPAT_FIXED)   // scan queries (no segment tree)
+        return neu ? (src ? MODE_FIX_MIXED_POISSON : MODE_FIX_MIXED) : (src ? MODE_FIX_POISSON : MODE_FIX_DIRICHLET);
     const bool tree = neu && use_tree(h);
     if (h->delta) return neu ? (tree ? MODE_MIXED_DELTA_TREE : MODE_MIXED_DELTA) : MODE_DELTA;
     if (neu) return src ? (tree ? MODE_MIXED_POISSON_TREE : MODE_MIXED_POISSON) : (tree ? MODE_MIXED_TREE : MODE_MIXED);
@@ -437,11 +441,12 @@ namespace {
 // HIP call; the handle's device is -1 until wost_create takes a device.
 int create_host(const wost_problem* pb, wost_handle** out) {
     *out = nullptr;
-    if (pb->compat != WOST_COMPAT_REFERENCE) {
-        if (pb->compat == WOST_COMPAT_FIXED)
-            return fail(WOST_ERR_UNSUPPORTED, "compat='fixed' is not available in ABI version %d", WOST_ABI_VERSION);
+    if (pb->compat != WOST_COMPAT_REFERENCE && pb->compat != WOST_COMPAT_FIXED)
         return fail(WOST_ERR_INVALID_ARG, "unknown compat %d", pb->compat);
-    }
+    if (pb->compat == WOST_COMPAT_FIXED && (pb->sigma || pb->alpha))
+        return fail(WOST_ERR_UNSUPPORTED,
+                    "compat='fixed' covers the Laplace, Poisson and mixed estimators; delta tracking (sigma/alpha, "
+                    "quirks Q4/Q5) runs with compat='reference' only");
     wost_handle* h = new wost_handle();
     h->device = -1;
     int rc;

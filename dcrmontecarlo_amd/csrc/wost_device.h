@@ -682,6 +682,50 @@ WOST_HD float2 segment_left_normal(float2 sa, float2 sb) {
     return float2{-ey, ex};
 }
 
+// compat="fixed" ray query (quirk Q1 corrected): the nearest crossing along
+// the ray, i.e. the least RAY parameter t over the segments the reference's
+// test accepts (s in [0, 1], t > 0), a hit when t <= r at q + t d. The
+// reference returns the least SEGMENT parameter instead (ray_segment_time).
+template <class VP>
+WOST_HD Hit intersect_polylines_ray(VP v, int nv, float px, float py, float dxi, float dyi, float r) {
+#pragma clang fp contract(off)
+    Hit h;
+    float dn, dx, dy;
+    unit_direction(dxi, dyi, dn, dx, dy);
+    if (dn < 1e-10f) {
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
+        return h;
+    }
+    const float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
+    float best = WOST_INF;
+    int bi = -1;
+    float2 a = v[0];
+    for (int i = 1; i < nv; ++i) {
+        const float2 b = v[i];
+        const float ux = b.x - a.x, uy = b.y - a.y;
+        const float wx = qx - a.x, wy = qy - a.y;
+        const float den = dx * uy - dy * ux;
+        const float rd = f_rcp(den);
+        const float ns = dx * wy - dy * wx, nt = ux * wy - uy * wx;
+        const float sa = ns * rd, ta = nt * rd;
+        if (sa >= -1e-6f && sa <= 1.000001f && ta > -1e-6f && ta < best * 1.000001f + 1e-30f) {
+            const float s = ns / den, t = nt / den;
+            if (s >= 0.0f && s <= 1.0f && t > 0.0f && t < best) { best = t; bi = i - 1; }
+        }
+        a = b;
+    }
+    if (bi < 0 || best > r) {
+        h.x = px + r * dx; h.y = py + r * dy; h.nx = 0.f; h.ny = 0.f; h.hit = false; h.seg = -1;
+        return h;
+    }
+    h.x = qx + best * dx;
+    h.y = qy + best * dy;
+    h.nx = 0.f; h.ny = 0.f;
+    h.hit = true;
+    h.seg = bi;
+    return h;
+}
+
 // :179-197 -- the hit (or miss) from the winning segment bi and its "time".
 // NORMAL = false leaves the normal out (the walk kernels look up the
 // segment's precomputed normal angle by h.seg instead).

@@ -348,7 +348,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
       << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
       << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
-      << (n_sources > 1 ? ", " + std::to_string(n_sources) : std::string()) << ">(A, fld, smem);\n}\n";
+      << ", " << n_sources << ", " << (mode_fix(mode) ? "true" : "false") << ">(A, fld, smem);\n}\n";
     return o.str();
 }
 

@@ -122,41 +122,45 @@ struct InterpFields {
 // One walk-step of _solveUnified (solvers/WoStSolver.py:206-291) for every
 // active lane, with the finish/refill logic of loops 1-2 (:182-188, :294-311)
 // around it: see wost_walk.h.
-template <bool NEU, bool SRC, bool DELTA, bool TREE>
+template <bool NEU, bool SRC, bool DELTA, bool TREE, bool FIX>
 __global__ void __launch_bounds__(kWalkBlock, WOST_WALK_MIN_WAVES)
 wost_walk_kernel(const WalkArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const InterpFields fld(A.prog);
-    walk_body<NEU, SRC, DELTA, TREE, true>(A, fld, smem);   // records when A.rec is set
+    walk_body<NEU, SRC, DELTA, TREE, true, 1, FIX>(A, fld, smem);   // records when A.rec is set
 }
 
 // mode -> kernel instantiation (MODE_* of wost_internal.h)
 #define WOST_FOR_MODE(mode, X)                                   \
     switch (mode) {                                              \
-    case MODE_DIRICHLET: X(false, false, false, false);          \
-    case MODE_POISSON: X(false, true, false, false);             \
-    case MODE_MIXED: X(true, false, false, false);               \
-    case MODE_MIXED_POISSON: X(true, true, false, false);        \
-    case MODE_DELTA: X(false, true, true, false);                \
-    case MODE_MIXED_DELTA: X(true, true, true, false);           \
-    case MODE_MIXED_TREE: X(true, false, false, true);           \
-    case MODE_MIXED_POISSON_TREE: X(true, true, false, true);    \
-    case MODE_MIXED_DELTA_TREE: X(true, true, true, true);       \
+    case MODE_DIRICHLET: X(false, false, false, false, false);        \
+    case MODE_POISSON: X(false, true, false, false, false);           \
+    case MODE_MIXED: X(true, false, false, false, false);             \
+    case MODE_MIXED_POISSON: X(true, true, false, false, false);      \
+    case MODE_DELTA: X(false, true, true, false, false);              \
+    case MODE_MIXED_DELTA: X(true, true, true, false, false);         \
+    case MODE_MIXED_TREE: X(true, false, false, true, false);         \
+    case MODE_MIXED_POISSON_TREE: X(true, true, false, true, false);  \
+    case MODE_MIXED_DELTA_TREE: X(true, true, true, true, false);     \
+    case MODE_FIX_DIRICHLET: X(false, false, false, false, true);     \
+    case MODE_FIX_POISSON: X(false, true, false, false, true);        \
+    case MODE_FIX_MIXED: X(true, false, false, false, true);          \
+    case MODE_FIX_MIXED_POISSON: X(true, true, false, false, true);   \
     default: return hipErrorInvalidValue;                        \
     }
 
 hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu) {
     const size_t lds = walk_lds_bytes(mode, nd, nn, n_points);
-#define OCC(n, s, d, t) \
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<n, s, d, t>, kWalkBlock, lds)
+#define OCC(n, s, d, t, x) \
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<n, s, d, t, x>, kWalkBlock, lds)
     WOST_FOR_MODE(mode, OCC)
 #undef OCC
 }
 
 hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s) {
     const size_t lds = walk_lds_bytes(mode, a.nd, a.nn, a.n_points);
-#define LAUNCH(n, sr, d, t)                                                 \
-    wost_walk_kernel<n, sr, d, t><<<grid, kWalkBlock, lds, s>>>(a); \
+#define LAUNCH(n, sr, d, t, x)                                       \
+    wost_walk_kernel<n, sr, d, t, x><<<grid, kWalkBlock, lds, s>>>(a); \
     return hipGetLastError()
     WOST_FOR_MODE(mode, LAUNCH)
 #undef LAUNCH

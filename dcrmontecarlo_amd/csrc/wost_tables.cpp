@@ -149,6 +149,21 @@ void greens_sampler_nodes(float* out, int n) {
     }
 }
 
+void greens_sampler_nodes_jacobian(float* out, int n) {
+    auto cdf = [](double rho) { return rho * rho * (1.0 - 2.0 * std::log(rho)); };
+    for (int i = 0; i < n; ++i) {
+        const double u = (double)i / (double)(n - 1);
+        if (i == 0) { out[i] = 0.0f; continue; }
+        if (i == n - 1) { out[i] = 1.0f; continue; }
+        double lo = 0.0, hi = 1.0;
+        for (int it = 0; it < 200 && hi - lo > 1e-17; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            if (cdf(mid) < u) lo = mid; else hi = mid;
+        }
+        out[i] = (float)(0.5 * (lo + hi));
+    }
+}
+
 void screened_sampler_nodes(float* out, int n, double sigma_bar) {
     const double a = 1e-6;
     const int J = 1 << 16;

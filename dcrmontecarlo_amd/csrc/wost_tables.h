@@ -38,6 +38,10 @@ void greens_phi(double x, double* phi, double* dphi);
 //  * ScreenedGreensDistribution2D (solvers/utils.py:181-195): density
 //    min(|G_sigmabar(rho; R=1)|, screenedGreensNorm2D(1, sigma_bar)) on [1e-6, 1).
 void greens_sampler_nodes(float* out, int n);
+// compat="fixed" (quirk Q3 corrected): the radial density of a point sampled
+// from the ball's Green's function in 2-D, rho ln(1/rho) on (0, 1) (the
+// Jacobian rho included); F(rho) = rho^2 (1 + 2 ln(1/rho)).
+void greens_sampler_nodes_jacobian(float* out, int n);
 void screened_sampler_nodes(float* out, int n, double sigma_bar);
 
 }  // namespace wost

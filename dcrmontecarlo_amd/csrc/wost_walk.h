@@ -88,12 +88,24 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // source's total is bit for bit what a single-source solve of it gives. The
 // Fields policy then provides f_multi(x, y, float out[NS]); per-walk values go
 // to out_val[local walk * NS + k].
-template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, class F>
+// FIX (compat="fixed", Laplace / Poisson / mixed): the estimator with the
+// reference's quirks corrected:
+//  Q7/Q12 the walk stops when the CURRENT point's Dirichlet distance is <= eps
+//         (no extra step inside the eps-shell; eps >= 1 no longer skips walks);
+//  Q1     the Neumann ray query takes the nearest crossing along the ray;
+//  Q2     after a Neumann hit the direction is uniform on the hemisphere of the
+//         INWARD normal (the side the ray came from);
+//  Q3     the source radius follows the Green's density with its Jacobian,
+//         rho ln(1/rho) (the host builds that sampler table);
+//  Q13    the source sample takes its own direction (Philox word w) and counts
+//         only if it is visible from x (no Neumann crossing before it).
+template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, bool FIX = false, class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
     // the walk's position updates round op by op like the reference (torch CPU
     // has no FMA contraction); the field math it calls keeps its own setting
 #pragma clang fp contract(off)
     static_assert(NS >= 1 && (NS == 1 || SRC) && (NS == 1 || !REC), "multi-source walks need a source, no recorder");
+    static_assert(!(FIX && (DELTA || TREE)), "compat=fixed covers the Laplace, Poisson and mixed scan estimators");
     float2* sD = reinterpret_cast<float2*>(smem);
     float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
     float* sPhi = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
@@ -195,7 +207,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 if (points_in_lds) q = sP[pid];
                 else q = A.points[pid];
                 px = q.x; py = q.y;
-                k = 0; dD = 1.0f; onB = false; phi = 0.f; w = 1.f;
+                k = 0; dD = FIX ? WOST_INF : 1.0f; onB = false; phi = 0.f; w = 1.f;
 #pragma unroll
                 for (int s = 0; s < NS; ++s) total[s] = 0.f;
                 if (DELTA) ax = fld.alpha(px, py);
@@ -211,6 +223,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 
         // --- one walk-step (:206-291)
         const float dd = fld.dirichlet_distance(sD, A.nd, px, py);  // :208
+        if (FIX && !(dd > A.eps)) {   // Q7/Q12 fixed: stop here, g at this point
+            dD = dd;
+            continue;
+        }
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
         if (NEU) {
@@ -228,15 +244,22 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float theta = (u01(rn.x) * 2.0f) * kPiF;                     // :226
         // :227-228 (quirk Q2): atan2(normal) is a property of the segment that
         // was hit, precomputed per segment with the same device atan2f
-        if (NEU && onB) theta = theta / 2.0f + phi;
+        if (NEU && onB) theta = FIX ? theta / 2.0f + (phi - kPiF / 2.0f) : theta / 2.0f + phi;
         const float cs = f_cos(theta), sn = f_sin(theta);            // :230-232
 
         float xnx, xny;
         if (NEU) {                                                   // :235-236
-            const Hit h = TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
-                               : fld.neumann_intersect(sN, A.nn, px, py, cs, sn, r);
+            const Hit h = FIX ? intersect_polylines_ray(sN, A.nn, px, py, cs, sn, r)
+                              : TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
+                                     : fld.neumann_intersect(sN, A.nn, px, py, cs, sn, r);
             xnx = h.x; xny = h.y; onB = h.hit;
             if (h.hit) phi = TREE ? A.seg_phi[h.seg] : sPhi[h.seg];
+            if (FIX && h.hit) {
+                // inward normal: the left normal when the ray crossed the segment from
+                // its left side, i.e. cross(d, u) > 0 (then dot(left normal, d) < 0)
+                const float2 a = sN[h.seg], b = sN[h.seg + 1];
+                if (!(cs * (b.y - a.y) - sn * (b.x - a.x) > 0.0f)) phi = phi + kPiF;
+            }
         } else {                                                     // :238-239
             xnx = px + r * cs;
             xny = py + r * sn;
@@ -249,16 +272,24 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         Jet aj{0.f, 0.f, 0.f, 0.f};
         if (SRC) {                                                   // :242-258
             const float rs = sample_rho(sT, u01(rn.y)) * r;          // :244 (sampler, quirks Q3-Q5)
-            yx = px + rs * cs;                                       // :245 (quirk Q13)
-            yy = py + rs * sn;
-            const float e1x = yx - px, e1y = yy - py;
-            const float e2x = xnx - px, e2y = xny - py;
-            // :248 compares the two norms. sqrt is monotone, so sqrt(a2) > sqrt(b2)
-            // needs a2 > b2 (rare: only Neumann hits make the next point closer);
-            // only then evaluate the reference's exact comparison.
-            const float a2 = e1x * e1x + e1y * e1y, b2 = e2x * e2x + e2y * e2y;
-            if (a2 > b2) clipped = sqrtf(a2) > sqrtf(b2);
-            if (clipped) { yx = xnx; yy = xny; }
+            if constexpr (FIX) {                                     // Q13 fixed: own direction
+                const float ts = (u01(rn.w) * 2.0f) * kPiF;
+                const float cs2 = f_cos(ts), sn2 = f_sin(ts);
+                yx = px + rs * cs2;
+                yy = py + rs * sn2;
+                if (NEU) clipped = intersect_polylines_ray(sN, A.nn, px, py, cs2, sn2, rs).hit;   // not visible
+            } else {
+                yx = px + rs * cs;                                   // :245 (quirk Q13)
+                yy = py + rs * sn;
+                const float e1x = yx - px, e1y = yy - py;
+                const float e2x = xnx - px, e2y = xny - py;
+                // :248 compares the two norms. sqrt is monotone, so sqrt(a2) > sqrt(b2)
+                // needs a2 > b2 (rare: only Neumann hits make the next point closer);
+                // only then evaluate the reference's exact comparison.
+                const float a2 = e1x * e1x + e1y * e1y, b2 = e2x * e2x + e2y * e2y;
+                if (a2 > b2) clipped = sqrtf(a2) > sqrtf(b2);
+                if (clipped) { yx = xnx; yy = xny; }
+            }
             if (DELTA) {
                 gnorm = greens_norm_from_table(sG, r * sqrt_sb, r, inv_sb);   // solvers/utils.py:29-44
                 aj = fld.alpha_jet(yx, yy);

@@ -101,7 +101,7 @@ def _problem(dxy, nxy, g, f, sigma, alpha, compat, device, sigma_bar):
 
 
 def kernel_source(dirichletBoundary, dirichletBoundaryFunction=None, neumannBoundary=None, source=None,
-                  sigma=None, alpha=None, *, sigma_bar: float | None = None) -> str:
+                  sigma=None, alpha=None, *, sigma_bar: float | None = None, compat: str = "reference") -> str:
     """HIP source of the field-specialised walk kernel a WostSolver_2D with these
     arguments would compile (no device needed; wost_kernel_source)."""
     dxy = np.asarray(_np(dirichletBoundary.points), dtype=np.float32).reshape(-1, 2)
@@ -113,7 +113,9 @@ def kernel_source(dirichletBoundary, dirichletBoundaryFunction=None, neumannBoun
     a = conv(alpha, "alpha", is_alpha=True)
     if a is not None and a.is_constant():
         a = detach(a)
-    prob, keep = _problem(dxy, nxy, g, f, s, a, "reference", 0, sigma_bar)
+    if compat not in _lib.COMPAT:
+        raise ValueError(f"compat must be one of {sorted(_lib.COMPAT)}")
+    prob, keep = _problem(dxy, nxy, g, f, s, a, compat, 0, sigma_bar)
     n = ctypes.c_int64(0)
     _lib.check(_lib.lib.wost_kernel_source(ctypes.byref(prob), None, 0, ctypes.byref(n)), "wost_kernel_source")
     buf = ctypes.create_string_buffer(n.value + 1)
