@@ -83,6 +83,7 @@ WOST_HD float f_exp(float x) { return __expf(x); }
 WOST_HD float f_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 WOST_HD float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 WOST_HD float f_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+WOST_HD float f_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
 WOST_HD float f_sin(float x) { return __sinf(x); }
 WOST_HD float f_cos(float x) { return __cosf(x); }
 #else
@@ -90,6 +91,7 @@ WOST_HD float f_exp(float x) { return expf(x); }
 WOST_HD float f_rcp(float x) { return 1.0f / x; }
 WOST_HD float f_div(float a, float b) { return a / b; }
 WOST_HD float f_sqrt(float x) { return sqrtf(x); }
+WOST_HD float f_rsq(float x) { return 1.0f / sqrtf(x); }
 WOST_HD float f_sin(float x) { return sinf(x); }
 WOST_HD float f_cos(float x) { return cosf(x); }
 #endif
@@ -240,11 +242,12 @@ WOST_HD Jet fj_sigmoid_lin(float x, float y, float a, float b, float c) {
 }
 WOST_HD Jet fj_sigmoid_radial(float x, float y, float k, float cx, float cy, float R) {
     float dx = x - cx, dy = y - cy;
-    float d = f_sqrt(dx * dx + dy * dy);
+    float d2 = dx * dx + dy * dy;
+    float inv = f_rsq(d2);             // one transcendental for d and 1/d
+    float d = d2 > 0.f ? d2 * inv : 0.f;
     float s = sigmoidf(k * (d - R));
     float s1 = s * (1.f - s);          // ds/dz
     float s2 = s1 * (1.f - 2.f * s);   // d2s/dz2
-    float inv = f_rcp(d);
     // z = k (d - R): grad z = k (x-c)/d, lap z = k/d (2-D), |grad z|^2 = k^2
     return Jet{s, s1 * k * dx * inv, s1 * k * dy * inv, s2 * k * k + s1 * k * inv};
 }

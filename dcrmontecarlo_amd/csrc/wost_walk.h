@@ -299,7 +299,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 if (!clipped) {
                     const float f = fld.f(yx, yy);
                     if (DELTA)
-                        c = (f * gnorm) * f_rcp(f_sqrt(aj.v * ax)) * w;  // :253-254
+                        c = (f * gnorm) * f_rsq(aj.v * ax) * w;  // :253-254
                     else
                         c = f * ((r * r) / 4.0f);                        // :256, utils.py:61
                 }
@@ -308,7 +308,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             } else if (!clipped) {                                       // the same per source
                 float fv[NS];
                 fld.f_multi(yx, yy, fv);
-                const float sa = DELTA ? f_rcp(f_sqrt(aj.v * ax)) : 0.0f;
+                const float sa = DELTA ? f_rsq(aj.v * ax) : 0.0f;
                 const float q = DELTA ? 0.0f : ((r * r) / 4.0f);
 #pragma unroll
                 for (int s = 0; s < NS; ++s) {
