@@ -75,7 +75,7 @@ def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
             "sample": f"dcr_dipole {len(pts)} electrodes x {w} walks ({int(s.sum())} walk-steps, {dt:.1f} s), "
                       f"oracle/wost_oracle.c with {threads} OpenMP threads"}
     # the same oracle on one core, on a smaller sample (all cores and one core)
-    w1 = max(16, int(w * threads * 0.25 / 16))
+    w1 = max(16, int(w * 0.06))
     t0 = time.perf_counter()
     _, s1 = pb.solve_walks(pts, w1, sc.max_steps, sc.eps, CPU_SEED + 1, threads=1)
     dt1 = time.perf_counter() - t0

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--only", default="")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--compat", default="reference", help="reference | fixed (non-delta scenarios only)")
     a = ap.parse_args()
     names = a.only.split(",") if a.only else list(SIZES)
     out = {}
@@ -32,7 +33,9 @@ def main():
         npts, W = SIZES[name]
         W = max(1, int(W * a.scale))
         sc = S.ALL[name]()
-        solver = sc.solver(device=int(os.environ.get("LOCAL_RANK", "0")))
+        if a.compat != "reference" and (sc.sigma is not None or sc.alpha is not None):
+            continue
+        solver = sc.solver(device=int(os.environ.get("LOCAL_RANK", "0")), compat=a.compat)
         pts = sc.points[:npts]
         solver.solve(pts, nWalks=max(1, W // 10), maxSteps=sc.max_steps, eps=sc.eps, seed=1)   # warm-up
         best = None
