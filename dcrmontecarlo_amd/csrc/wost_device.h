@@ -532,7 +532,8 @@ WOST_HD float poly_distance(VP v, int nv, float px, float py) {
 template <class VP>
 WOST_HD float poly_distance_const(VP v, const float* rcp, int nv, float px, float py) {
 #pragma clang fp contract(off)
-    bool redo = !(fabsf(px) <= 0x1p60f && fabsf(py) <= 0x1p60f);
+    bool redo = !(fabsf(px) <= 0x1p60f && fabsf(py) <= 0x1p60f);   // also catches NaN
+    float qmin = WOST_INF, qmax = 0.0f;   // range of |q| over the Markstein segments
     float best = WOST_INF;
     float2 a = v[0];
     for (int i = 1; i < nv; ++i) {
@@ -547,8 +548,8 @@ WOST_HD float poly_distance_const(VP v, const float* rcp, int nv, float px, floa
             t = duv / duu;
         } else {
             const float q = duv * y;
-            const float aq = fabsf(q);
-            redo |= !(aq >= 0x1p-40f && aq <= 0x1p40f);
+            qmin = fminf(qmin, fabsf(q));   // q is not NaN: px, py are finite here
+            qmax = fmaxf(qmax, fabsf(q));
             t = fmaf(fmaf(-q, duu, duv), y, q);
         }
         t = fminf(fmaxf(t, 0.0f), 1.0f);
@@ -558,6 +559,7 @@ WOST_HD float poly_distance_const(VP v, const float* rcp, int nv, float px, floa
         best = fminf(best, ex * ex + ey * ey);
         a = b;
     }
+    redo |= !(qmin >= 0x1p-40f && qmax <= 0x1p40f);
     float d = sqrtf(best);
     if (WOST_ANY(redo)) {
         if (redo) d = poly_distance(v, nv, px, py);
@@ -614,8 +616,13 @@ WOST_HD float ray_segment_time(float2 a, float2 b, float qx, float qy, float dx,
 // The same test with the two IEEE divisions done only for candidate segments.
 // The candidate filter uses the hardware reciprocal and is a strict superset
 // of the reference's validity (slack 1e-6 on s >= 0 / s <= 1, t >= 0), and the
-// candidates are then decided with the exact divisions, so the result is bit
-// for bit that of ray_segment_time.
+// candidates are then decided with the exact division for s, and t > 0 by the
+// signs of nt and den: that is t's sign unless the quotient could round to 0
+// (|nt/den| < 2^-150), which |ta| >= 2^-120 rules out; otherwise (rare, under
+// a wave vote) by the division. den = +-0 makes s non-finite, so the segment
+// is rejected whatever t says. The result is bit for bit that of
+// ray_segment_time. (Hoisting the rare division out of the segment loop, as a
+// redo of the whole scan, measured slower: profiles/r01_final/ab_raytest.log.)
 WOST_HD float ray_segment_time_filtered(float2 a, float2 b, float qx, float qy, float dx, float dy) {
 #pragma clang fp contract(off)
     float ux = b.x - a.x, uy = b.y - a.y;
@@ -628,8 +635,12 @@ WOST_HD float ray_segment_time_filtered(float2 a, float2 b, float qx, float qy, 
     float res = WOST_INF;
     if (sa >= -1e-6f && sa <= 1.000001f && ta >= 0.0f) {
         float s = ns / den;
-        float t = nt / den;
-        if ((s >= 0.0f) && (s <= 1.0f) && (t > 0.0f)) res = s;
+        bool tpos = (nt > 0.0f) == (den > 0.0f);
+        const bool tiny = !(fabsf(ta) >= 0x1p-120f);
+        if (WOST_ANY(tiny)) {
+            if (tiny) tpos = (nt / den) > 0.0f;
+        }
+        if ((s >= 0.0f) && (s <= 1.0f) && tpos) res = s;
     }
     return res;
 }
@@ -658,9 +669,11 @@ WOST_HD void unit_direction(float dxi, float dyi, float& dn, float& dx, float& d
 #else
     const bool fast = (uint32_t)(k + 64) <= 128u && fabsf(dxi) >= 0x1p-100f && fabsf(dyi) >= 0x1p-100f;
 #endif
-    const int32_t j = k >= 0 ? (k >> 1) : -((1 - k) >> 1);
+    // branch-free selects (the compiler otherwise splits the wave here)
+    const int32_t kneg = k >> 31, j = ((k >> 1) & ~kneg) | (-((1 - k) >> 1) & kneg);
+    const int32_t jneg = j >> 31;
     const float n = bits_to_float(0x3F800000 + j);
-    const float y = bits_to_float(j >= 0 ? 0x3F800000 - 2 * j : 0x3F800000 + ((1 - j) >> 1));
+    const float y = bits_to_float(0x3F800000 + ((-2 * j) & ~jneg) + (((1 - j) >> 1) & jneg));
     const float qx = dxi * y, qy = dyi * y;
     dn = n;
     dx = fmaf(fmaf(-qx, n, dxi), y, qx);

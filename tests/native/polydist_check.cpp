@@ -53,3 +53,20 @@ extern "C" int polydist_check(const float* verts, int nv, const float* pts, long
     *mismatches = bad;
     return 0;
 }
+
+// ray_segment_time_filtered (candidate filter, sign-only t test) against
+// ray_segment_time (both IEEE divisions), bit for bit: segs[n][4], rays[n][4].
+extern "C" int raytime_check(const float* segs, const float* rays, long n, long* mismatches, long* valid) {
+    long bad = 0, ok = 0;
+    for (long k = 0; k < n; ++k) {
+        const float2 a{segs[4 * k], segs[4 * k + 1]}, b{segs[4 * k + 2], segs[4 * k + 3]};
+        const float qx = rays[4 * k], qy = rays[4 * k + 1], dx = rays[4 * k + 2], dy = rays[4 * k + 3];
+        const float s0 = wost::ray_segment_time(a, b, qx, qy, dx, dy);
+        const float s1 = wost::ray_segment_time_filtered(a, b, qx, qy, dx, dy);
+        if (fb(s0) != fb(s1)) ++bad;
+        ok += s0 != WOST_INF;
+    }
+    *mismatches = bad;
+    *valid = ok;
+    return 0;
+}

@@ -74,3 +74,33 @@ def test_poly_distance_const_is_bitwise_poly_distance(lib, name):
     assert bad.value == 0
     if name in ("dcr_box", "variable_coefficients", "random0", "random1"):
         assert nm.value > 0   # the Markstein division is exercised
+
+
+def test_filtered_ray_test_is_bitwise_ray_test(lib):
+    """ray_segment_time_filtered (hardware-reciprocal candidate filter, then the
+    exact s and a sign-only t > 0 test) against both IEEE divisions
+    (PolylinesSimple.py:104-132), on random, grazing, tiny-t and degenerate cases."""
+    rng = np.random.default_rng(7)
+    n = 400_000
+    a = rng.normal(size=(n, 2)) * 10.0 ** rng.uniform(-3, 3, (n, 1))
+    b = a + rng.normal(size=(n, 2)) * 10.0 ** rng.uniform(-6, 2, (n, 1))
+    b[: n // 50] = a[: n // 50]                                            # zero-length segments
+    q = rng.normal(size=(n, 2)) * 10.0 ** rng.uniform(-3, 3, (n, 1))
+    m = n // 4                                                             # rays starting on / near the segment
+    t = rng.random(m)
+    q[:m] = a[:m] + t[:, None] * (b[:m] - a[:m]) + rng.normal(size=(m, 2)) * 10.0 ** rng.uniform(-40, -3, (m, 1))
+    ang = rng.uniform(0, 2 * np.pi, n)
+    d = np.stack([np.cos(ang), np.sin(ang)], 1)
+    u = b - a
+    par = slice(m, 2 * m)                                                  # (nearly) parallel rays
+    d[par] = u[par] / np.maximum(np.linalg.norm(u[par], axis=1, keepdims=True), 1e-30)
+    d[par] += rng.normal(size=(m, 2)) * 1e-7
+    segs = np.ascontiguousarray(np.concatenate([a, b], 1).astype(np.float32))
+    rays = np.ascontiguousarray(np.concatenate([q, d], 1).astype(np.float32))
+    lib.raytime_check.argtypes = [ctypes.POINTER(ctypes.c_float)] * 2 + [ctypes.c_long] + \
+        [ctypes.POINTER(ctypes.c_long)] * 2
+    bad, valid = ctypes.c_long(-1), ctypes.c_long(0)
+    p = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    assert lib.raytime_check(p(segs), p(rays), n, ctypes.byref(bad), ctypes.byref(valid)) == 0
+    assert bad.value == 0
+    assert valid.value > n // 20
