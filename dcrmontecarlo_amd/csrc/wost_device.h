@@ -53,13 +53,22 @@ WOST_HD void mulhilo(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
     lo = (uint32_t)p;
 }
 
+// a ^ b ^ c in one instruction on gfx950 (v_bitop3_b32, truth table 0x96)
+WOST_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 WOST_HD U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         uint32_t hi0, lo0, hi1, lo1;
         mulhilo(0xD2511F53u, c.x, hi0, lo0);
         mulhilo(0xCD9E8D57u, c.z, hi1, lo1);
-        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        c = U4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
