@@ -331,17 +331,22 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 
         if (DELTA) {                                                 // :271-284
             const float mu = u01(rn.z);
-            if (mu > sigma_bar * gnorm) {
-                const float an = clipped ? aj.v : fld.alpha(xnx, xny);
-                w = w * f_sqrt(f_div(an, ax));                       // :277
-                px = xnx; py = xny; ax = an;
-            } else {
+            const bool accept = mu > sigma_bar * gnorm;              // :273-275
+            // the two branches share the weight update w * sqrt(a_new / alpha(x));
+            // only the field evaluations stay divergent
+            float anew = aj.v;                                       // collision, or a clipped accept
+            if (accept && !clipped) anew = fld.alpha(xnx, xny);      // :277
+            float sc = 1.0f;
+            if (!accept) {
                 const float spv = sigma_prime_from(aj, fld.sigma(yx, yy), fld.detached());  // :281
-                float sc = 1.0f - spv * inv_sb;
+                sc = 1.0f - spv * inv_sb;
                 sc = (0.0f > sc) ? 0.0f : sc;                        // Python max(., 0.0) (:282)
-                w = (w * f_sqrt(f_div(aj.v, ax))) * sc;              // :283
-                px = yx; py = yy; ax = aj.v;
             }
+            const float wt = w * f_sqrt(f_div(anew, ax));           // :277 / :283
+            w = accept ? wt : wt * sc;
+            px = accept ? xnx : yx;
+            py = accept ? xny : yy;
+            ax = anew;
         } else {
             px = xnx; py = xny;                                      // :287
         }
