@@ -299,7 +299,9 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     // a short Dirichlet polyline is compiled in: the scan unrolls, the segment
     // vectors and squared lengths fold to constants (the same IEEE operations)
     o << "    __device__ __forceinline__ float dirichlet_distance(const float2* sD, int nd, float x, float y) const {\n";
-    if (nd <= kJitMaxConstVertices) {
+    int max_const = kJitMaxConstVertices;   // A/B knob: WOST_JIT_CONST_VERTICES (an integer)
+    if (const char* e = std::getenv("WOST_JIT_CONST_VERTICES")) max_const = std::max(0, std::min(256, std::atoi(e)));
+    if (nd <= max_const) {
         o << "        const float2 v[" << nd << "] = {";
         for (int i = 0; i < nd; ++i) o << (i ? ", " : "") << "{" << lit(dverts[2 * i]) << ", " << lit(dverts[2 * i + 1]) << "}";
         o << "};\n";
@@ -322,7 +324,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "        return wost::poly_distance(sD, nd, x, y);\n";
     }
     o << "    }\n";
-    const bool nconst = neu && !tree && nn >= 1 && nn <= kJitMaxConstVertices;
+    const bool nconst = neu && !tree && nn >= 1 && nn <= max_const;
     auto nverts_decl = [&]() {
         std::ostringstream v;
         v << "        const float2 v[" << nn << "] = {";

@@ -20,7 +20,7 @@ namespace wost {
 
 // Polylines of at most this many vertices are compiled into the specialised
 // kernel as constants.
-constexpr int kJitMaxConstVertices = 16;
+constexpr int kJitMaxConstVertices = 40;
 
 // HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
 // (wost_internal.h WalkMode) with the fields of `prog` and short polylines
