@@ -53,13 +53,40 @@ def _point_stats(v, W):
     return v.mean(axis=1), v.std(axis=1, ddof=1) / np.sqrt(W)
 
 
+def host_cpu() -> dict:
+    """The host's CPU model and the cores this process may run on."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "affinity_cpus": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+            "cgroup_cpu_quota": quota, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
     """The CPU oracle (C, OpenMP over walks) on a bounded sample of the same survey:
-    timed on the model solve (the cpu_baseline), then also run on the homogeneous
-    background so the sample yields the survey's apparent resistivities."""
+    timed on the model solve (the cpu_baseline) on every core this process may use,
+    then on one core, then also run on the homogeneous background so the sample
+    yields the survey's apparent resistivities."""
     from oracle import oracle as O
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    info = host_cpu()
+    threads = info["affinity_cpus"]
+    if info["cgroup_cpu_quota"]:                   # a CPU quota caps the usable cores below the affinity set
+        threads = max(1, min(threads, int(round(info["cgroup_cpu_quota"]))))
     pb = O.Problem.from_scenario(sc, sigma_bar=sigma_bar)
     pts = sc.points
     pb.solve_walks(pts, 2, sc.max_steps, sc.eps, 1, threads=threads)       # builds the sampler table
@@ -73,7 +100,8 @@ def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
         w = int(min(1_000_000, w * max(2.0, 0.8 * budget_s / max(dt, 1e-3))))
     base = {"value": float(s.sum()) / dt, "unit": "walk-steps/s", "cores": threads, "kind": "port",
             "sample": f"dcr_dipole {len(pts)} electrodes x {w} walks ({int(s.sum())} walk-steps, {dt:.1f} s), "
-                      f"oracle/wost_oracle.c with {threads} OpenMP threads"}
+                      f"oracle/wost_oracle.c with {threads} OpenMP threads (every usable host core)",
+            "host": info}
     # the same oracle on one core, on a smaller sample (all cores and one core)
     w1 = max(16, int(w * 0.06))
     t0 = time.perf_counter()
@@ -87,8 +115,10 @@ def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
 
 
 def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu):
-    """Apparent resistivity of the dipole-dipole line: the full GPU run's precision, and
-    the GPU vs the CPU reference on the same walks (same seeds) of the CPU sample."""
+    """Apparent resistivity of the dipole-dipole line: the full GPU run's precision, the
+    full GPU run against the reference's own run (tests/golden/rho_dcr_dipole.npz: the
+    north-star RMSE <= 1 sigma check), and the GPU vs the CPU port (oracle) on the same
+    walks (same seeds) of the CPU sample."""
     pairs = survey.dipole_dipole_pairs(len(gpu_full[0][0]))
 
     def rho(model, bg):
@@ -103,11 +133,14 @@ def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu):
            "gpu_full": {"walks_per_electrode": int(gpu_full[2]), "resolved": int(ok.sum()),
                         "mc_1sigma_rms": float(np.sqrt(np.mean(full.se[ok] ** 2))) if ok.any() else None,
                         "rho_a_checksum": float(np.sum(full.rho_a[ok]))}}
+    ref = survey.reference_rho_a(os.path.join(REPO, "tests", "golden", "rho_dcr_dipole.npz"))
+    if ref is not None and len(ref.rho.rho_a) == len(full.rho_a):
+        out["vs_reference"] = survey.compare_to_reference(full, ref)
     if cpu_same is not None:
         g, c = rho(*gpu_same), rho(*cpu_same)
         cmp = survey.compare(g, c)
         cmp_full = survey.compare(full, c)
-        out["vs_cpu_reference"] = {
+        out["vs_cpu_port"] = {
             "walks_per_electrode": int(w_cpu), "seed": CPU_SEED, "resolved": cmp["resolved"],
             "rmse": cmp["rmse"], "cpu_mc_1sigma_rms": cmp["mc_1sigma"],
             "rmse_over_1sigma": (cmp["rmse"] / cmp["mc_1sigma"]) if cmp["rmse"] is not None and cmp["mc_1sigma"] else None,
@@ -127,6 +160,21 @@ def measured_traffic():
             return json.load(f)["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         return None
+
+
+def issue_line(perfmodel, kernel_steps_per_s: float):
+    """The VALU issue-rate roofline of the walk kernel: instructions per wave-step from
+    the committed rocprofv3 PMC passes of this workload (profiles/issue_dcr_dipole.json),
+    at this run's kernel walk-steps/s."""
+    try:
+        with open(os.path.join(REPO, "profiles", "issue_dcr_dipole.json")) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    out = perfmodel.issue_fraction(pmc["valu_per_wave_step"], pmc["trans_per_wave_step"], kernel_steps_per_s)
+    out.update({"valu_per_wave_step": pmc["valu_per_wave_step"], "trans_per_wave_step": pmc["trans_per_wave_step"],
+                "pmc_source": pmc.get("source")})
+    return out
 
 
 def main():
@@ -205,7 +253,7 @@ def main():
     sc_h = survey.homogeneous(sc, ALPHA_BG)
     solver_h = sums_h = None
     if not args.no_rho:
-        solver_h = sc_h.solver(device=local)
+        solver_h = survey.homogeneous_solver(sc, ALPHA_BG, solver, device=local)
         sums_h, _ = one_step(args.steps - 1, solver_h)
 
     if rank == 0:
@@ -237,10 +285,11 @@ def main():
                                       "block sums"},
             "roofline": {"bound": "valu", "achieved": ach_tflops, "peak": perfmodel.FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": ach_tflops / perfmodel.FP32_PEAK_TFLOPS, "traffic": None,
-                         "model_flops_per_step": fps,
+                         "model_flops_per_step": fps, "flop_model": "SURVEY.md 8(d) v1 per-config total (C4 ~350)",
                          "kernel": "wost_walk_jit (hiprtc field-specialised, mixed+delta)" if jit
                          else "wost_walk_kernel<true,true,true> (precompiled)",
-                         "kernel_ms_per_launch": kernel_ms / max(launches, 1)},
+                         "kernel_ms_per_launch": kernel_ms / max(launches, 1),
+                         "issue": issue_line(perfmodel, steps_local / (kernel_ms * 1e-3) if kernel_ms > 0 else 0.0)},
             "roofline_hbm": {"bound": "hbm", "achieved": ach_gbs, "peak": perfmodel.HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": ach_gbs / perfmodel.HBM_PEAK_GBS, "traffic": measured_traffic(),
                              "algorithmic_bytes_per_launch": bytes_per_launch},
@@ -250,7 +299,7 @@ def main():
         w_cpu = 0
         if not args.no_cpu and world == 1:
             if solver_h is None:
-                solver_h = sc_h.solver(device=local)
+                solver_h = survey.homogeneous_solver(sc, ALPHA_BG, solver, device=local)
             base, w_cpu, cm, ch = cpu_leg(sc, sc_h, solver.sigma_bar or 0.0, solver_h.sigma_bar or 0.0,
                                           args.cpu_seconds)
             out["cpu_baseline"] = base

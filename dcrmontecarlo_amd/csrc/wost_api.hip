@@ -325,6 +325,17 @@ double estimate_sigma_bar(const wost_handle* h, const Program& prog) {
     return sb;
 }
 
+// The largest float x with sqrtf(x) <= rmin (IEEE sqrt, as the kernels take it): a
+// silhouette vertex at squared distance <= x makes r = max(rmin, min(dn, dd)) equal
+// rmin whatever the other vertices are (silhouette_distance_tree's early stop).
+float silhouette_stop2(float rmin) {
+    if (!(rmin > 0.0f) || !std::isfinite(rmin)) return -1.0f;
+    float x = rmin * rmin;
+    while (x > 0.0f && std::sqrt(x) > rmin) x = std::nextafter(x, 0.0f);
+    while (std::sqrt(std::nextafter(x, INFINITY)) <= rmin) x = std::nextafter(x, INFINITY);
+    return x;
+}
+
 bool use_tree(const wost_handle* h) {
     const int nseg = (int)(h->nverts.size() / 2) - 1;
     return nseg >= 1 && h->tree_min_segments >= 0 && nseg >= h->tree_min_segments;
@@ -347,8 +358,10 @@ int ensure_tree(wost_handle* h) {
         return fail(WOST_ERR_INVALID_ARG, "cannot build the Neumann segment tree");
     if (h->d_tree) (void)hipFree(h->d_tree);
     h->d_tree = nullptr;
-    HIP_TRY(hipMalloc(&h->d_tree, sizeof(float) * h->tree.node.size()));
-    HIP_TRY(hipMemcpy(h->d_tree, h->tree.node.data(), sizeof(float) * h->tree.node.size(), hipMemcpyHostToDevice));
+    const size_t n = std::max<size_t>(h->tree.rec.size(), 16);
+    HIP_TRY(hipMalloc(&h->d_tree, sizeof(float) * n));
+    if (!h->tree.rec.empty())
+        HIP_TRY(hipMemcpy(h->d_tree, h->tree.rec.data(), sizeof(float) * h->tree.rec.size(), hipMemcpyHostToDevice));
     h->tree_ready = true;
     return WOST_OK;
 }
@@ -724,6 +737,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_first_leaf = h->tree.first_leaf;
         a.tree_leaf = h->tree.leaf;
         a.tree_tol = h->tree.tol;
+        a.tree_stop2 = silhouette_stop2(a.rmin);
     }
 
     std::vector<int64_t> begins;

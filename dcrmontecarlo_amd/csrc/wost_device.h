@@ -806,22 +806,32 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
 // :134-197); these queries return the same bits while visiting only the parts
 // of the polyline that can matter.
 //
-// Implicit complete binary tree (built by wost_api.hip, build_segment_tree):
+// Implicit complete binary tree (built by wost_tree.cpp, build_segment_tree):
 // node k has children 2k+1 and 2k+2; leaves are nodes first_leaf.. and leaf l
 // owns segments [l*L, min((l+1)*L, nseg)). A node's range of segments also
 // includes the first segment of its right neighbour (a vertex's silhouette
-// test reads both adjacent segments). node[2k] is the node's bounding box
+// test reads both adjacent segments). A node is described by its bounding box
 // (xmin, ymin, xmax, ymax) of the range's vertices, exact (min/max of vertex
-// coordinates); node[2k+1] is the arc of its segment directions as its two
-// edge unit vectors (e1, e2), see cone_excludes_silhouettes. Padding leaves
-// have inverted boxes.
+// coordinates), and the arc of its segment directions as its two edge unit
+// vectors (e1, e2), see cone_excludes_silhouettes. Padding leaves have
+// inverted boxes.
+//
+// Layout (BVH2 child records): internal node k stores its two CHILDREN's
+// descriptions in one 64-byte record rec[4k .. 4k+3] = {box(2k+1),
+// box(2k+2), cone(2k+1), cone(2k+2)}, so one step of a traversal tests both
+// children with four independent loads (one memory round trip per level).
+// The first `n_lds` records may be staged in LDS (TREE kernels: `lds`), the
+// rest are read from global memory. Traversals keep no stack: a bit per level
+// records a pending second child (and, for the nearest-first silhouette
+// search, which child it is); the ancestor at depth p of node k at depth d is
+// ((k + 1) >> (d - p)) - 1.
 //
 // Exactness:
 //  * the ray query prunes nodes whose box is farther than tol from the ray's
 //    LINE (behind or ahead); a segment the float test accepts lies within a few
 //    ulps of the line (tol is ~2^-14 of the coordinates, 10^3 times that), and
-//    leaves are visited in ascending segment order, so `s < best` keeps the
-//    first argmin like the scan;
+//    leaves are visited in ascending segment order (left child first), so
+//    `s < best` keeps the first argmin like the scan;
 //  * the silhouette query prunes by a box lower bound on the squared distance,
 //    which rounds monotonically (contraction off) to at most any vertex's
 //    computed distance, and by the direction cone: when every segment
@@ -829,33 +839,36 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
 //    view vector, all cross products c1, c2 of :63-81 have one sign and no
 //    vertex of the node is a silhouette. Vertices farther than the Dirichlet distance dd
 //    (+0.2%) cannot change min(dn, dd) (:212), so they are pruned too and the
-//    result is exact for that use.
+//    result is exact for that use. The visiting order (nearer lower bound
+//    first) only decides how soon `best` tightens the bound.
 // ---------------------------------------------------------------------------
 struct SegTree {
-    const float4* node;   // [2 * n_nodes]
+    const float4* rec;    // [4 * first_leaf] child records (global memory)
+    const float4* lds;    // the first n_lds records staged in LDS (or null)
+    int n_lds;
     const float2* v;      // polyline vertices
     int nv;               // vertex count
-    int first_leaf;       // index of the first leaf node
+    int first_leaf;       // index of the first leaf node (= number of internal nodes)
     int leaf;             // segments per leaf
     float tol;            // line-test tolerance at the origin; grows with |q|
+    WOST_HD const float4* record(int k) const { return k < n_lds ? lds + 4 * k : rec + 4 * k; }
 };
 
 constexpr float kConeMargin = 1e-3f;
 
 #if defined(WOST_TREE_STATS) && !defined(__HIP_DEVICE_COMPILE__)
-extern long g_tree_stats[4];   // host harness only: silhouette nodes, leaves; ray nodes, leaves
+extern long g_tree_stats[4];   // host harness only: silhouette records, leaves; ray records, leaves
 #define WOST_TREE_COUNT(i) (++g_tree_stats[i])
 #else
 #define WOST_TREE_COUNT(i) ((void)0)
 #endif
 
-WOST_HD int tree_near_child(const SegTree& t, int k, float px, float py) {
-#pragma clang fp contract(off)
-    const float4 a = t.node[2 * (2 * k + 1)], b = t.node[2 * (2 * k + 2)];
-    const float ax = 0.5f * (a.x + a.z) - px, ay = 0.5f * (a.y + a.w) - py;
-    const float bx = 0.5f * (b.x + b.z) - px, by = 0.5f * (b.y + b.w) - py;
-    // an inverted (padding) right child has a NaN centre and is never nearer
-    return (bx * bx + by * by < ax * ax + ay * ay) ? 2 * k + 2 : 2 * k + 1;
+WOST_HD int highest_bit(uint32_t m) {   // m != 0
+#if defined(__HIP_DEVICE_COMPILE__)
+    return 31 - __clz((int)m);
+#else
+    return 31 - __builtin_clz(m);
+#endif
 }
 
 // True when no vertex of the node can be a silhouette seen from p. The cone
@@ -887,41 +900,55 @@ WOST_HD bool cone_excludes_silhouettes(float4 box, float4 cone, float px, float 
     return lo > m || hi < -m;
 }
 
-template <class Prune, class Visit>
-WOST_HD void tree_scan(const SegTree& t, Prune prune, Visit visit) {
-    // left-to-right stackless traversal: leaves come in ascending segment order
-    int k = 0;
-    for (;;) {
-        if (!prune(k)) {
-            if (k < t.first_leaf) { k = 2 * k + 1; continue; }
-            visit(k - t.first_leaf);
-        }
-        while (k > 0 && (k & 1) == 0) k = (k - 1) >> 1;   // right child: climb
-        if (k == 0) return;
-        ++k;                                              // left child: its sibling
-    }
+// Squared distance from p to the box (a lower bound of every vertex's computed
+// squared distance), +inf for an inverted (padding) box.
+WOST_HD float box_lower_bound2(float4 b, float px, float py) {
+#pragma clang fp contract(off)
+    const float gx = fmaxf(fmaxf(b.x - px, px - b.z), 0.0f);
+    const float gy = fmaxf(fmaxf(b.y - py, py - b.w), 0.0f);
+    return b.x > b.z ? WOST_INF : gx * gx + gy * gy;
 }
 
-// silhouette_distance for the use min(dn, dd) of :212: exact when the result
-// is below dd; otherwise some value >= dd (or +inf).
-WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, float dd) {
+WOST_HD bool silhouette_keep(float4 box, float4 cone, float lb, float bound, float px, float py) {
+    return !(lb > bound) && !cone_excludes_silhouettes(box, cone, px, py);
+}
+
+// silhouette_distance for the use r = max(rmin, min(dn, dd)) of :210-212: exact
+// when the result is below dd and above rmin; otherwise some value >= dd (or
+// +inf), or some value <= rmin. stop2 is the largest float whose sqrtf is <= rmin
+// (host: silhouette_stop2), or a negative value for no early stop: once a
+// silhouette vertex with d2 <= stop2 is found, min(dn, dd) <= rmin whatever the
+// others are, so r = rmin and the search ends.
+WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, float dd, float stop2 = -1.0f) {
 #pragma clang fp contract(off)
     float best = WOST_INF;
     const int nv = t.nv, nseg = nv - 1;
     if (nv < 3) return best;
     const float T = (dd * dd) * 1.002f;
-    int k = 0;
+    int k = 0, depth = 0;
+    uint32_t pend = 0u, far_right = 0u;   // per level: second child pending / it is the right one
     for (;;) {
-        WOST_TREE_COUNT(0);
-        const float4 b = t.node[2 * k];
-        const float gx = fmaxf(fmaxf(b.x - px, px - b.z), 0.0f);
-        const float gy = fmaxf(fmaxf(b.y - py, py - b.w), 0.0f);
-        const float lb = gx * gx + gy * gy;
-        const float bound = best < T ? best : T;
-        bool skip = lb > bound || b.x > b.z;
-        if (!skip) skip = cone_excludes_silhouettes(b, t.node[2 * k + 1], px, py);
-        if (!skip) {
-            if (k < t.first_leaf) { k = tree_near_child(t, k, px, py); continue; }
+        bool climb = true;
+        if (k < t.first_leaf) {
+            WOST_TREE_COUNT(0);
+            const float4* r = t.record(k);
+            const float4 bl = r[0], br = r[1], cl = r[2], cr = r[3];
+            const float bound = best < T ? best : T;
+            const float lbl = box_lower_bound2(bl, px, py), lbr = box_lower_bound2(br, px, py);
+            const bool okl = silhouette_keep(bl, cl, lbl, bound, px, py);
+            const bool okr = silhouette_keep(br, cr, lbr, bound, px, py);
+            if (okl || okr) {
+                const bool near_right = okr && (!okl || lbr < lbl);
+                const uint32_t bit = 1u << depth;
+                if (okl && okr) {
+                    pend |= bit;
+                    far_right = near_right ? (far_right & ~bit) : (far_right | bit);
+                }
+                k = 2 * k + 1 + (near_right ? 1 : 0);
+                ++depth;
+                climb = false;
+            }
+        } else {
             WOST_TREE_COUNT(1);
             const int s0 = (k - t.first_leaf) * t.leaf;
             const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
@@ -938,15 +965,25 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
                     va = vb;
                     vb = vc;
                 }
+                if (best <= stop2) return sqrtf(best);
             }
         }
-        // next node: the parent's other child if k was visited first, else climb
-        for (;;) {
-            if (k == 0) return best == WOST_INF ? best : sqrtf(best);
-            const int parent = (k - 1) >> 1;
-            if (k == tree_near_child(t, parent, px, py)) { k = (k & 1) ? k + 1 : k - 1; break; }
-            k = parent;
+        if (!climb) continue;
+        // resume the deepest pending second child, re-tested against the tightened bound
+        bool resumed = false;
+        while (pend != 0u) {
+            const int p = highest_bit(pend);
+            pend &= ~(1u << p);
+            const int anc = ((k + 1) >> (depth - p)) - 1;
+            const int side = (int)((far_right >> p) & 1u);
+            const float4* r = t.record(anc);
+            const float4 b = r[side], c = r[2 + side];
+            const float bound = best < T ? best : T;
+            k = 2 * anc + 1 + side;
+            depth = p + 1;
+            if (silhouette_keep(b, c, box_lower_bound2(b, px, py), bound, px, py)) { resumed = true; break; }
         }
+        if (!resumed) return best == WOST_INF ? best : sqrtf(best);
     }
 }
 
@@ -966,27 +1003,47 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
     const int nseg = t.nv - 1;
     float best = WOST_INF;
     int bi = -1;
-    tree_scan(
-        t,
-        [&](int k) {
+    // a box farther than tol from the ray's line holds no segment the float test accepts
+    auto line_keep = [&](float4 b) {
+        const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
+        const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
+        return !(b.x > b.z || fabsf(dx * cy - dy * cx) > fabsf(dx) * hy + fabsf(dy) * hx + tol);
+    };
+    int k = 0, depth = 0;
+    uint32_t pend = 0u;   // per level: the right child is pending
+    for (;;) {
+        bool climb = true;
+        if (k < t.first_leaf) {
             WOST_TREE_COUNT(2);
-            const float4 b = t.node[2 * k];
-            const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
-            const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
-            return b.x > b.z || fabsf(dx * cy - dy * cx) > fabsf(dx) * hy + fabsf(dy) * hx + tol;
-        },
-        [&](int l) {
-            WOST_TREE_COUNT(3);
-            const int s0 = l * t.leaf;
-            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
-            float2 a = t.v[s0];
-            for (int i = s0; i < s1; ++i) {
-                const float2 b = t.v[i + 1];
-                const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
-                if (s < best) { best = s; bi = i; }
-                a = b;
+            const float4* rr = t.record(k);
+            const bool okl = line_keep(rr[0]), okr = line_keep(rr[1]);
+            if (okl || okr) {
+                if (okl && okr) pend |= 1u << depth;
+                k = 2 * k + (okl ? 1 : 2);   // left first: leaves in ascending segment order
+                ++depth;
+                climb = false;
             }
-        });
+        } else {
+            WOST_TREE_COUNT(3);
+            const int s0 = (k - t.first_leaf) * t.leaf;
+            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+            if (s0 < s1) {
+                float2 a = t.v[s0];
+                for (int i = s0; i < s1; ++i) {
+                    const float2 b = t.v[i + 1];
+                    const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
+                    if (s < best) { best = s; bi = i; }
+                    a = b;
+                }
+            }
+        }
+        if (!climb) continue;
+        if (pend == 0u) break;
+        const int p = highest_bit(pend);
+        pend &= ~(1u << p);
+        k = 2 * (((k + 1) >> (depth - p)) - 1) + 2;   // the right child of the depth-p ancestor
+        depth = p + 1;
+    }
     return intersect_finish<NORMAL>(t.v, bi, best, px, py, dx, dy, qx, qy, r);
 }
 

@@ -42,7 +42,7 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
     const int n_nodes = 2 * P - 1;
     out->first_leaf = P - 1;
     out->leaf = leaf;
-    out->node.assign(8 * (size_t)n_nodes, 0.f);
+    std::vector<float> node(8 * (size_t)n_nodes, 0.f);   // per node: box, cone
 
     // segment range [lo, hi] of every node (hi includes the right neighbour's
     // first segment: a vertex's silhouette test reads both adjacent segments)
@@ -68,7 +68,7 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
 
     std::vector<double> ang;
     for (int k = 0; k < n_nodes; ++k) {
-        float* box = &out->node[8 * (size_t)k];
+        float* box = &node[8 * (size_t)k];
         float* cone = box + 4;
         if (lo[k] < 0) {   // padding: inverted box, "no segment" cone
             box[0] = inf; box[1] = inf; box[2] = -inf; box[3] = -inf;
@@ -98,6 +98,18 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
             cone[1] = (float)std::sin(axis - half);
             cone[2] = (float)std::cos(axis + half);
             cone[3] = (float)std::sin(axis + half);
+        }
+    }
+    // child records of the internal nodes: {box(2k+1), box(2k+2), cone(2k+1), cone(2k+2)}
+    out->rec.assign(16 * (size_t)(P - 1), 0.f);
+    for (int k = 0; k < P - 1; ++k) {
+        float* r = &out->rec[16 * (size_t)k];
+        for (int c = 0; c < 2; ++c) {
+            const float* nd = &node[8 * (size_t)(2 * k + 1 + c)];
+            for (int q = 0; q < 4; ++q) {
+                r[4 * c + q] = nd[q];          // box
+                r[8 + 4 * c + q] = nd[4 + q];  // cone
+            }
         }
     }
     return true;

@@ -8,8 +8,9 @@
 namespace wost {
 
 struct SegmentTreeHost {
-    std::vector<float> node;   // 8 floats per node: box (xmin, ymin, xmax, ymax), direction-arc edges (e1, e2)
-    int first_leaf = 0;        // index of the first leaf node
+    std::vector<float> rec;    // 16 floats per internal node k: its children's boxes (xmin, ymin, xmax, ymax)
+                               // then their direction-arc edges (e1, e2): box(2k+1), box(2k+2), cone(2k+1), cone(2k+2)
+    int first_leaf = 0;        // index of the first leaf node = number of internal nodes
     int leaf = 0;              // segments per leaf
     float tol = 0.f;           // line-test tolerance at the origin
 };

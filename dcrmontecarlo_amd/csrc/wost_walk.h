@@ -47,7 +47,7 @@ struct WalkArgs {
     int32_t tree_first_leaf;
     int32_t tree_leaf;
     float tree_tol;
-    int32_t pad_;
+    float tree_stop2;            // largest float whose sqrtf is <= rmin (< 0: none); silhouette_distance_tree
 };
 
 constexpr int kWalkBlock = 256;
@@ -121,7 +121,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
         for (int i = threadIdx.x; i < A.nn - 1; i += blockDim.x) sPhi[i] = A.seg_phi[i];
     }
-    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_leaf, A.tree_tol};
+    const SegTree tree{A.tree, nullptr, 0, A.nverts, A.nn, A.tree_first_leaf, A.tree_leaf, A.tree_tol};
     if (SRC)
         for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
     if (DELTA) {
@@ -230,7 +230,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
         if (NEU) {
-            const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd)
+            const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
                                   : fld.neumann_silhouette_distance(sN, A.nn, px, py);  // :211
             dnv = dn;
             const float m = dn < dd ? dn : dd;                       // Python min()

@@ -122,7 +122,21 @@ class PolyLinesSimple(PolyLines):
     @staticmethod
     def funcToPolyline(func, x_min: float, x_max: float, resolution: float) -> "PolyLinesSimple":
         """Heightmap -> polyline. Like the reference (:226-240) the samples start at
-        x = 0 and x_min is ignored (quirk Q11)."""
+        x = 0 and x_min is ignored (quirk Q11). ``func`` receives what the reference
+        gives it, a float32 torch tensor torch.arange(0, x_max, resolution), when torch
+        is importable (the polyline's points are then a torch tensor, as there), and
+        the same values as a float32 numpy array otherwise."""
+        try:
+            import torch
+        except ImportError:
+            torch = None
+        if torch is not None:
+            x = torch.arange(0, x_max, resolution)
+            y = func(x)
+            if not isinstance(y, torch.Tensor):
+                y = torch.as_tensor(np.asarray(y, dtype=np.float32))
+            return PolyLinesSimple(torch.stack((x, y.to(x.dtype)), dim=-1))
+        # ATen's CPU arange: n = ceil((end - start) / step), x_i = start + i * step in double
         n = int(np.ceil((float(x_max) - 0.0) / float(resolution)))
         x = (np.arange(max(n, 0), dtype=np.float64) * float(resolution)).astype(np.float32)
         y = np.asarray(func(x), dtype=np.float32)

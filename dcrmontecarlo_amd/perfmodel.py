@@ -1,35 +1,54 @@
 """Algorithmic work model of one walk-step (for roofline reporting).
 
 A walk-step is one iteration of the reference's while loop
-(solvers/WoStSolver.py:206-291). Its floating-point work is counted from the
-operations that loop performs -- not from the instructions the compiler emits
--- with the SURVEY.md 8d convention: add/sub/mul = 1, FMA = 2,
-div/sqrt/exp/log/sin/cos/atan2 = 1 each, comparisons and the Philox integer
-work = 0. Per component (derivations in DESIGN.md, "Roofline"):
+(solvers/WoStSolver.py:206-291). The roofline fraction in bench.py uses
+SURVEY.md 8(d)'s FLOP model v1 verbatim (convention: add/mul = 1, FMA = 2,
+sqrt/rcp/exp/log/sin/cos = 1, compares and Philox integer work = 0):
 
-  closest point on a segment (PolylinesSimple.py:37-47)        23 per Dirichlet segment, +1 sqrt
-  silhouette test of an interior vertex (:63-81)               15 per Neumann interior vertex
-  ray-segment test (:117-130)                                  15 per Neumann segment, +14 setup/exit
-  direction theta, cos, sin (WoStSolver.py:226-232)             4
-  next point without Neumann (:238)                             4
-  source sample, clip test (:244-250)                          22
-  Poisson contribution f r^2/4 (:256-258)                       4 + f
-  delta: Green's norm via i0e Chebyshev (utils.py:43-44)       74
-  delta: contribution (:253-258)                                6 + f + jet(alpha)
-  delta: collision update incl. sigma' (:271-284)              28 + sigma
-Field costs: per term 3, per factor value / jet as in _FACTOR_VALUE / _FACTOR_JET.
+  F_geom = 12 S_D + 15 (V_N - 2)^+ + 14 S_N
+           (closest point per Dirichlet segment, silhouette test per interior
+            Neumann vertex, ray test per Neumann segment)
+  F_mode = Laplace ~10 | Poisson ~25 + f | delta ~150 (i0e ~120 included) + fields
+
+with the per-config totals SURVEY 8(d) quotes:
+
+  C1a Laplace ~58, C2 Poisson ~75, C3 variable coefficients ~1,150,
+  C4 DCR ~350, C5 brute force ~290,000
+
+The kernel no longer evaluates the i0e series (the Green's norm is an LDS
+table lookup), so for delta tracking the model counts ~120 FLOP
+the kernel does not execute; the fraction is reported against SURVEY's model
+anyway, so that it is reproducible from SURVEY 8(d) and nothing else.
+
+For configurations SURVEY does not quote, ``flops_per_step`` evaluates the same
+v1 formula with the fields costed per term / factor (``_field_cost``).
 """
 from __future__ import annotations
 
-# per-factor costs (value, jet incl. the product-rule multiply)
+# SURVEY.md 8(d) "Per config (FLOP/step)"
+SURVEY_FLOPS = {
+    "laplace_square": 58.0,
+    "poisson_square": 75.0,
+    "variable_coefficients": 1150.0,
+    "dcr_dipole": 350.0,
+    "dcr_dipole_homogeneous": 350.0,
+    "wenner_topography": 290000.0,
+}
+
+# per-factor costs (value, jet incl. the product-rule multiply), for fields of
+# configurations SURVEY 8(d) does not quote
 _FACTOR_VALUE = {1: None, 2: 16, 3: 5, 4: 5, 5: 8, 6: 12, 7: 4, 8: 5, 9: 58}
 _FACTOR_JET = {1: None, 2: 50, 3: 32, 4: 32, 5: 36, 6: 50, 7: 24, 8: 25, 9: 160}
-# 9 (tabulated): per axis 16 for the Catmull-Rom weights (+18 derivatives, +12
-# second derivatives for the jet); 4 rows x 4 taps multiply-add = 32 (x3 for the
-# jet) plus the 4-row combination
 
 FP32_PEAK_TFLOPS = 157.3      # MI355X vector (= dense MFMA) FP32, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec
+# issue model (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'): a wave64
+# VALU instruction occupies its SIMD for 2 cycles, a transcendental
+# (v_exp/log/rcp/rsq/sqrt/sin/cos) for 8
+CLOCK_GHZ = 2.4
+N_SIMDS = 256 * 4
+VALU_ISSUE_CYC = 2.0
+TRANS_ISSUE_CYC = 8.0
 
 
 def _field_cost(field, jet: bool) -> float:
@@ -47,40 +66,42 @@ def _field_cost(field, jet: bool) -> float:
     return total
 
 
-TREE_MIN_SEGMENTS = 64       # include/wost.h WOST_TREE_MIN_SEGMENTS_DEFAULT
-
-
-def flops_per_step(scenario):
-    """Model FLOPs of one walk-step of the scenario's kernel variant, or None when
-    the Neumann queries go through the segment tree: its work depends on the
-    traversal, and the reference's full-scan count would exceed the peak."""
-    if scenario.neumann is not None and scenario.neumann.shape[0] - 1 >= TREE_MIN_SEGMENTS:
-        return None
-    nd = scenario.dirichlet.shape[0]
-    F = 23.0 * (nd - 1) + 1.0
-    neu = scenario.neumann is not None
-    if neu:
-        nn = scenario.neumann.shape[0]
-        F += 15.0 * max(nn - 2, 0) + 1.0
-        F += 15.0 * (nn - 1) + 14.0
-    else:
-        F += 4.0
-    F += 4.0
+def flops_per_step(scenario) -> float:
+    """SURVEY 8(d) v1 FLOPs of one walk-step: the quoted per-config total when
+    SURVEY quotes one for this scenario, else the v1 formula."""
+    if scenario.name in SURVEY_FLOPS:
+        return SURVEY_FLOPS[scenario.name]
+    sd = scenario.dirichlet.shape[0] - 1
+    F = 12.0 * sd
+    if scenario.neumann is not None:
+        vn = scenario.neumann.shape[0]
+        F += 15.0 * max(vn - 2, 0) + 14.0 * (vn - 1)
     delta = scenario.sigma is not None or scenario.alpha is not None
-    if scenario.f is not None:
-        F += 22.0 + _field_cost(scenario.f, jet=False)
-        if delta:
-            F += 74.0 + 6.0 + _field_cost(scenario.alpha, jet=True)
-            F += 28.0 + _field_cost(scenario.sigma, jet=False)
-        else:
-            F += 4.0
+    if delta:
+        F += 150.0 + _field_cost(scenario.f, False) + _field_cost(scenario.alpha, True) \
+            + _field_cost(scenario.sigma, False)
+    elif scenario.f is not None:
+        F += 25.0 + _field_cost(scenario.f, False)
+    else:
+        F += 10.0
     return F
+
+
+def issue_fraction(valu_per_wave_step: float, trans_per_wave_step: float, steps_per_s: float) -> dict:
+    """VALU issue-rate roofline: the SIMD cycles one wave-step's instructions occupy,
+    (VALU - TRANS) x 2 + TRANS x 8, times the wave-steps per second, over the chip's
+    SIMD cycles per second."""
+    cyc = (valu_per_wave_step - trans_per_wave_step) * VALU_ISSUE_CYC + trans_per_wave_step * TRANS_ISSUE_CYC
+    avail = N_SIMDS * CLOCK_GHZ * 1e9
+    used = cyc * steps_per_s / 64.0
+    return {"bound": "valu-issue", "cycles_per_wave_step": cyc, "achieved_simd_cycles_per_s": used,
+            "peak_simd_cycles_per_s": avail, "frac": used / avail,
+            "ceiling_walk_steps_per_s": avail * 64.0 / cyc if cyc > 0 else None}
 
 
 def hbm_bytes_per_walk() -> float:
     """Algorithmic HBM traffic of the walk kernel per walk: the per-walk result
     (float value + uint32 step count) it writes. Geometry, sampler table, field
     program and query points are read once per workgroup into LDS / the scalar
-    cache. (rocprofv3 on C4: WRITE_SIZE 413 MB per 48M-walk launch, FETCH_SIZE
-    0.4 MB after the gfx950 x2 correction -- profiles/r01_jit/.)"""
+    cache."""
     return 8.0

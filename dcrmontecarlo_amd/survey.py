@@ -87,10 +87,89 @@ def apparent_resistivity(model: DipoleData, homogeneous: DipoleData, rho_bg: flo
 
 
 def homogeneous(sc: Scenario, alpha_bg: float) -> Scenario:
-    """The same survey with the conductivity field replaced by its background value."""
+    """The same survey with the conductivity field replaced by its background value.
+    Solve it with the model solver's sigma_bar (``homogeneous_solver``): the delta-
+    tracking collision test mu > sigma_bar G(r) and the sampler then match the
+    model's, so walks with the same seed take identical paths and only their
+    weights differ (common random numbers)."""
     return Scenario(sc.name + "_homogeneous", sc.dirichlet, sc.neumann, g=sc.g, f=sc.f, sigma=sc.sigma,
                     alpha=F.const(alpha_bg), points=sc.points, n_walks=sc.n_walks, max_steps=sc.max_steps,
                     eps=sc.eps, reference=sc.reference)
+
+
+def homogeneous_solver(sc: Scenario, alpha_bg: float, model_solver, **kw):
+    """WostSolver_2D of homogeneous(sc) with the model solver's sigma_bar (so that
+    model and background walks of one seed share their paths)."""
+    return homogeneous(sc, alpha_bg).solver(sigma_bar=model_solver.sigma_bar, **kw)
+
+
+def paired_apparent_resistivity(model_walks: np.ndarray, bg_walks: np.ndarray, pairs: np.ndarray,
+                                rho_bg: float) -> ApparentResistivity:
+    """rho_a from per-walk values [E, W] of the model and the background solved on
+    common random numbers (walk w of electrode e shares its path in both): the
+    delta-method standard error then includes the model/background covariance of
+    each electrode (electrodes are independent of each other)."""
+    m = np.asarray(model_walks, np.float64)
+    h = np.asarray(bg_walks, np.float64)
+    W = m.shape[1]
+    um, uh = m.mean(1), h.mean(1)
+    vm, vh = m.var(1, ddof=1) / W, h.var(1, ddof=1) / W
+    cmh = np.array([np.cov(m[e], h[e], ddof=1)[0, 1] for e in range(m.shape[0])]) / W
+    i, j = pairs[:, 0], pairs[:, 1]
+    A, B = um[i] - um[j], uh[i] - uh[j]
+    vA, vB, cAB = vm[i] + vm[j], vh[i] + vh[j], cmh[i] + cmh[j]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        R = A / B
+        var = (vA - 2.0 * R * cAB + R * R * vB) / (B * B)
+    rho = rho_bg * R
+    return ApparentResistivity(rho, rho_bg * np.sqrt(np.maximum(var, 0.0)), np.abs(B) > 3.0 * np.sqrt(vB))
+
+
+@dataclass
+class ReferenceSurvey:
+    rho: ApparentResistivity     # the reference's rho_a per dipole-dipole receiver
+    walks: int                   # walks per electrode the reference ran
+    common_paths: bool           # model and background walks shared their paths
+    u_model: np.ndarray          # [E] its electrode potentials
+    u_background: np.ndarray
+
+
+def reference_rho_a(path: str) -> ReferenceSurvey | None:
+    """The reference's own dipole-dipole apparent resistivities of the C4 survey
+    (tests/golden/rho_dcr_dipole.npz, made by tools/gen_fixtures.py --only rho: the
+    reference's _solveUnified with its own torch/numpy RNG at all 48 electrodes, model
+    conductivity and homogeneous alpha = 100), or None when the fixture is absent."""
+    try:
+        z = np.load(path, allow_pickle=False)
+    except OSError:
+        return None
+    m, h = z["model_values"], z["background_values"]
+    pairs = dipole_dipole_pairs(m.shape[0])
+    rho = paired_apparent_resistivity(m, h, pairs, 1.0 / float(z["alpha_bg"]))
+    return ReferenceSurvey(rho, int(z["n_walks"]), bool(z["common_paths"]), m.mean(1), h.mean(1))
+
+
+def compare_to_reference(gpu: ApparentResistivity, ref: ReferenceSurvey) -> dict:
+    """The north-star check (BASELINE.json): RMSE of rho_a(GPU) - rho_a(reference) over
+    the dipoles the reference resolves, against the reference's own 1-sigma Monte-Carlo
+    error there (RMS), plus z-scores with both errors (RMS z <= 1.2, max
+    |z| < 4). Dipoles the reference does not resolve are 'unpinned'."""
+    r = ref.rho
+    ok = r.resolved & gpu.resolved & np.isfinite(gpu.rho_a) & np.isfinite(r.rho_a)
+    out = {"reference_walks_per_electrode": ref.walks, "dipoles": int(len(r.rho_a)), "resolved": int(ok.sum()),
+           "unpinned": int(len(r.rho_a) - ok.sum()), "reference_common_paths": ref.common_paths}
+    if not ok.any():
+        out.update({"rmse": None, "ref_1sigma_rms": None, "rmse_over_1sigma": None, "z_rms": None, "z_max": None})
+        return out
+    d = gpu.rho_a[ok] - r.rho_a[ok]
+    s = np.sqrt(gpu.se[ok] ** 2 + r.se[ok] ** 2)
+    z = d / np.where(s > 0, s, 1.0)
+    rmse = float(np.sqrt(np.mean(d * d)))
+    one_sigma = float(np.sqrt(np.mean(r.se[ok] ** 2)))
+    out.update({"rmse": rmse, "ref_1sigma_rms": one_sigma, "rmse_over_1sigma": rmse / one_sigma if one_sigma else None,
+                "rmse_le_1sigma": bool(rmse <= one_sigma), "z_rms": float(np.sqrt(np.mean(z * z))),
+                "z_max": float(np.max(np.abs(z))), "resolved_dipoles": [int(i) for i in np.nonzero(ok)[0]]})
+    return out
 
 
 @dataclass
@@ -109,7 +188,8 @@ def run_dipole_dipole(sc: Scenario, alpha_bg: float, n_walks: int, seed: int = 0
     """Solve the survey on the GPU: electrode potentials of the model and of the
     homogeneous background (same walk streams), then dV and rho_a = (1/alpha_bg) dV/dV_bg."""
     if solvers is None:
-        solvers = (sc.solver(device=device), homogeneous(sc, alpha_bg).solver(device=device))
+        sm = sc.solver(device=device)
+        solvers = (sm, homogeneous_solver(sc, alpha_bg, sm, device=device))
     sm, sh = solvers
     _, st_m = sm.solve(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=seed, return_stats=True)
     _, st_h = sh.solve(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=seed, return_stats=True)
@@ -159,7 +239,8 @@ def run_dipole_dipole_survey(sc: Scenario, alpha_bg: float, n_walks: int, n_max:
     tx = np.unique(quad[:, :2], axis=0) if len(quad) else np.zeros((0, 2), np.int64)
     srcs = [dipole_source(sc.points[a], sc.points[b], width) for a, b in tx]
     if solvers is None:
-        solvers = (sc.solver(device=device), homogeneous(sc, alpha_bg).solver(device=device))
+        sm = sc.solver(device=device)
+        solvers = (sm, homogeneous_solver(sc, alpha_bg, sm, device=device))
     sm, sh = solvers
     out = []
     steps = 0

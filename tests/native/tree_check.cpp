@@ -44,8 +44,8 @@ int tree_check(const float* xy, int nv, int leaf, const float* pts, const float*
                const float* dd, long n, long* out) {
     SegmentTreeHost th;
     if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
-    const SegTree t{reinterpret_cast<const float4*>(th.node.data()), reinterpret_cast<const float2*>(xy), nv,
-                    th.first_leaf, th.leaf, th.tol};
+    const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), nullptr, 0, reinterpret_cast<const float2*>(xy),
+                    nv, th.first_leaf, th.leaf, th.tol};
     const float2* v = reinterpret_cast<const float2*>(xy);
     out[0] = out[1] = out[2] = out[3] = 0;
     for (long i = 0; i < n; ++i) {
@@ -62,6 +62,36 @@ int tree_check(const float* xy, int nv, int leaf, const float* pts, const float*
             ++out[1];
         if (hb.hit) ++out[3];
     }
+    return 0;
+}
+
+// The walk's use r = max(rmin, min(dn, dd)) (:210-215) with the tree's early stop
+// at stop2 (the largest float whose sqrtf is <= rmin) against the full scan.
+// out[0] = mismatches of r, out[1] = queries where the early stop decided r
+// (the scan found a silhouette at <= rmin), out[2] = tree node visits.
+int tree_check_stop(const float* xy, int nv, int leaf, const float* pts, const float* dd, float rmin, float stop2,
+                    long n, long* out) {
+    SegmentTreeHost th;
+    if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
+    const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), nullptr, 0, reinterpret_cast<const float2*>(xy),
+                    nv, th.first_leaf, th.leaf, th.tol};
+    const float2* v = reinterpret_cast<const float2*>(xy);
+    out[0] = out[1] = out[2] = 0;
+#if !defined(__HIP_DEVICE_COMPILE__)
+    for (int i = 0; i < 4; ++i) g_tree_stats[i] = 0;
+#endif
+    for (long i = 0; i < n; ++i) {
+        const float px = pts[2 * i], py = pts[2 * i + 1];
+        const float dn_b = silhouette_distance(v, nv, px, py);
+        const float dn_t = silhouette_distance_tree(t, px, py, dd[i], stop2);
+        const float mb = dn_b < dd[i] ? dn_b : dd[i], mt = dn_t < dd[i] ? dn_t : dd[i];
+        const float rb = mb > rmin ? mb : rmin, rt = mt > rmin ? mt : rmin;
+        if (!same(rb, rt)) ++out[0];
+        if (dn_b <= rmin) ++out[1];
+    }
+#if !defined(__HIP_DEVICE_COMPILE__)
+    out[2] = g_tree_stats[0];
+#endif
     return 0;
 }
 

@@ -33,7 +33,21 @@ def harness(tmp_path_factory):
     lib.tree_check.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, ctypes.c_long,
                                ctypes.POINTER(ctypes.c_long)]
     lib.tree_check.restype = ctypes.c_int
+    lib.tree_check_stop.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_float,
+                                    ctypes.c_long, ctypes.POINTER(ctypes.c_long)]
+    lib.tree_check_stop.restype = ctypes.c_int
     return lib
+
+
+def stop2_of(rmin):
+    """The largest float32 whose (correctly rounded) sqrt is <= rmin (wost_api.hip silhouette_stop2)."""
+    rmin = np.float32(rmin)
+    x = np.float32(rmin * rmin)
+    while x > 0 and np.sqrt(x) > rmin:
+        x = np.nextafter(x, np.float32(0))
+    while np.sqrt(np.nextafter(x, np.float32(np.inf))) <= rmin:
+        x = np.nextafter(x, np.float32(np.inf))
+    return x
 
 
 def run(lib, verts, pts, dirs, radii, dd, leaf=8):
@@ -88,6 +102,26 @@ def test_tree_matches_scan_full_topography(harness):
     verts = S.topography(10_000)
     counts = run(harness, verts, *queries(rng, verts, 60000))
     assert counts[0] == 0 and counts[1] == 0, counts
+
+
+@pytest.mark.parametrize("rmin", [0.45, 0.05, 2.0])
+def test_tree_early_stop_keeps_the_step_radius(harness, rmin):
+    """silhouette_distance_tree stops once a silhouette vertex lies within rmin: the
+    step radius max(rmin, min(dn, dd)) is then rmin whatever the rest of the polyline
+    holds. Checked against the full scan on near-surface points of the C5 topography."""
+    rng = np.random.default_rng(int(rmin * 100))
+    verts = S.topography(10_000)
+    pts, _, _, dd = queries(rng, verts, 40000)
+    stop2 = stop2_of(rmin)
+    assert np.sqrt(stop2) <= np.float32(rmin) < np.sqrt(np.nextafter(stop2, np.float32(np.inf)))
+    f = lambda a: np.ascontiguousarray(a, np.float32)
+    p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    out = (ctypes.c_long * 3)()
+    verts, pts, dd = f(verts), f(pts), f(dd)
+    assert harness.tree_check_stop(p(verts), verts.shape[0], 8, p(pts), p(dd), float(rmin), float(stop2),
+                                   pts.shape[0], out) == 0
+    assert out[0] == 0, list(out)
+    assert out[1] > 100, list(out)        # the early stop was exercised
 
 
 @pytest.mark.parametrize("shape", ["circle", "zigzag", "random_walk", "degenerate"])

@@ -481,11 +481,84 @@ def gen_stats(names, workers):
         print(f"stats_{name}.npz", f"{time.time() - t0:.1f}s", "mean steps", arr[:, 2].mean())
 
 
+# ---------------------------------------------------------------------------
+# G8: the C4 survey's electrode potentials with the reference's own RNG, for the
+# model conductivity and the homogeneous background (alpha = 100), all 48
+# electrodes -> the reference's apparent resistivities (BASELINE metric, part 2)
+# ---------------------------------------------------------------------------
+RHO_ALPHA_BG = 100.0        # tests/testGeophysicalScenario.py:43 background_conductivity
+
+
+def _rho_spec(field):
+    spec = ref_scenarios()["dcr_dipole"]()
+    if field == "background":
+        # the same conductivity function with its anomalies removed: a tensor-valued
+        # constant (the reference's sqrt(alpha(.)/alpha(.)) needs tensors, WoStSolver.py:277)
+        spec["alpha"] = lambda p: RHO_ALPHA_BG + 0.0 * p[0]
+    return spec
+
+
+def _rho_worker(args):
+    field, e, chunk, pt, W, ms, eps, seed = args
+    torch.set_num_threads(1)
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    solver = build_ref_solver(_rho_spec(field))
+    with _quiet(), contextlib.redirect_stderr(io.StringIO()):
+        u, hist = solver.solve(torch.from_numpy(pt), nWalks=W, maxSteps=ms, eps=eps, return_history=True)
+    v = np.array([sum(float(c["contribution"]) for c in wk["contributions"]) for wk in hist[0]], np.float64)
+    s = np.array([len(wk["path"]) for wk in hist[0]], np.int32)
+    return field, e, chunk, v, s, float(solver.sigma_bar)
+
+
+def gen_rho(walks, workers, chunk=50):
+    """Per-walk values of the reference at every C4 electrode (48 x walks), model and
+    background. Model and background use the same seed per (electrode, chunk): both have
+    sigma_bar = 10 (Q8 fallback) and draw the same torch/numpy numbers, so their walks take
+    identical paths (common random numbers, checked via the step counts) and only the
+    weights differ."""
+    import multiprocessing as mp
+
+    sc = S.dcr_dipole()
+    pts = np.ascontiguousarray(sc.points, np.float32)
+    E = len(pts)
+    nch = (walks + chunk - 1) // chunk
+    jobs = []
+    for c in range(nch):                  # chunk-major so partial progress covers every electrode
+        for e in range(E):
+            for field in ("model", "background"):
+                jobs.append((field, e, c, pts[e:e + 1], min(chunk, walks - c * chunk), sc.max_steps, sc.eps,
+                             100_000 + 1000 * e + c))
+    vals = {f: np.zeros((E, walks)) for f in ("model", "background")}
+    steps = {f: np.zeros((E, walks), np.int32) for f in ("model", "background")}
+    sbar = {}
+    t0 = time.time()
+    done = 0
+    with mp.get_context("fork").Pool(workers) as pool:
+        for field, e, c, v, s, sb in pool.imap_unordered(_rho_worker, jobs):
+            vals[field][e, c * chunk:c * chunk + len(v)] = v
+            steps[field][e, c * chunk:c * chunk + len(s)] = s
+            sbar[field] = sb
+            done += 1
+            if done % 48 == 0:
+                print(f"rho: {done}/{len(jobs)} jobs, {time.time() - t0:.0f}s", flush=True)
+    same = bool(np.array_equal(steps["model"], steps["background"]))
+    np.savez_compressed(os.path.join(OUT, "rho_dcr_dipole.npz"), points=pts, n_walks=np.int64(walks),
+                        max_steps=np.int64(sc.max_steps), eps=np.float32(sc.eps), alpha_bg=np.float64(RHO_ALPHA_BG),
+                        seeds=np.array([[100_000 + 1000 * e + c for c in range(nch)] for e in range(E)], np.int64),
+                        chunk=np.int64(chunk), model_values=vals["model"], background_values=vals["background"],
+                        model_steps=steps["model"], background_steps=steps["background"],
+                        sigma_bar_model=np.float64(sbar["model"]), sigma_bar_background=np.float64(sbar["background"]),
+                        common_paths=np.bool_(same))
+    print("rho_dcr_dipole.npz", f"{time.time() - t0:.0f}s", "common paths", same, "sigma_bar", sbar)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="geometry,fields,greens,sampler,replay,stats")
     ap.add_argument("--scenarios", default="")
     ap.add_argument("--stats-workers", type=int, default=8)
+    ap.add_argument("--rho-walks", type=int, default=400)
     a = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     parts = set(a.only.split(","))
@@ -503,6 +576,8 @@ def main():
         gen_replays(names)
     if "stats" in parts:
         gen_stats(names, a.stats_workers)
+    if "rho" in parts:
+        gen_rho(a.rho_walks, a.stats_workers)
 
 
 if __name__ == "__main__":
