@@ -114,7 +114,42 @@ def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
     return base, w, _point_stats(v, w), _point_stats(vh, w)
 
 
-def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu):
+RHO_SEED = 4242
+RHO_REPLICA_WALKS = 400      # the reference fixture's walks per electrode (tests/golden/rho_dcr_dipole.npz)
+RHO_REPLICAS = 512
+
+
+def paired_walks(survey, sc, solver, solver_h, n_walks):
+    """Per-walk values [E, W] of the model and of the homogeneous background on common
+    random numbers (same seed, same sigma_bar: identical paths, different weights)."""
+    vm, _ = solver.solve_walks(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=RHO_SEED)
+    vh, _ = solver_h.solve_walks(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=RHO_SEED)
+    return vm, vh
+
+
+def reference_leg(survey, alpha_bg, vm, vh):
+    """The GPU against the reference's own run (tests/golden/rho_dcr_dipole.npz): the
+    paired GPU estimate's RMSE vs the reference's 1 sigma (north star), z-scores, and
+    the matched-walk test -- is the reference's 400-walk rho_a a plausible draw of the
+    GPU estimator at 400 walks (512 independent replicas)?"""
+    ref = survey.reference_rho_a(os.path.join(REPO, "tests", "golden", "rho_dcr_dipole.npz"))
+    if ref is None or ref.rho.rho_a.shape[0] != vm.shape[0] - 1:
+        return None
+    pairs = survey.dipole_dipole_pairs(vm.shape[0])
+    gpu = survey.paired_apparent_resistivity(vm, vh, pairs, 1.0 / alpha_bg)
+    out = survey.compare_to_reference(gpu, ref)
+    out["gpu_walks_per_electrode"] = int(vm.shape[1])
+    rep = survey.replica_rho_a(vm, vh, pairs, 1.0 / alpha_bg, ref.walks)
+    p = survey.matched_walk_pvalues(rep, ref.rho.rho_a)
+    ok = np.isfinite(p)
+    out["matched_walks"] = {"replicas": int(rep.shape[0]), "walks_per_replica": int(ref.walks),
+                            "dipoles_tested": int(ok.sum()), "p_min": float(np.min(p[ok])) if ok.any() else None,
+                            "frac_p_gt_0.01": float(np.mean(p[ok] > 0.01)) if ok.any() else None}
+    out["gpu_paired_1sigma_rms"] = float(np.sqrt(np.mean(gpu.se[gpu.resolved] ** 2))) if gpu.resolved.any() else None
+    return out
+
+
+def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu, paired=None):
     """Apparent resistivity of the dipole-dipole line: the full GPU run's precision, the
     full GPU run against the reference's own run (tests/golden/rho_dcr_dipole.npz: the
     north-star RMSE <= 1 sigma check), and the GPU vs the CPU port (oracle) on the same
@@ -133,9 +168,8 @@ def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu):
            "gpu_full": {"walks_per_electrode": int(gpu_full[2]), "resolved": int(ok.sum()),
                         "mc_1sigma_rms": float(np.sqrt(np.mean(full.se[ok] ** 2))) if ok.any() else None,
                         "rho_a_checksum": float(np.sum(full.rho_a[ok]))}}
-    ref = survey.reference_rho_a(os.path.join(REPO, "tests", "golden", "rho_dcr_dipole.npz"))
-    if ref is not None and len(ref.rho.rho_a) == len(full.rho_a):
-        out["vs_reference"] = survey.compare_to_reference(full, ref)
+    if paired is not None:
+        out["vs_reference"] = reference_leg(survey, alpha_bg, *paired)
     if cpu_same is not None:
         g, c = rho(*gpu_same), rho(*cpu_same)
         cmp = survey.compare(g, c)
@@ -314,7 +348,8 @@ def main():
         if not args.no_rho:
             st_m, st_h = stats_from_sums(sums, Wt), stats_from_sums(sums_h, Wt)
             gpu_full = ((st_m.mean, st_m.stderr), (st_h.mean, st_h.stderr), Wt)
-            out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu)
+            paired = paired_walks(survey, sc, solver, solver_h, RHO_REPLICA_WALKS * RHO_REPLICAS)
+            out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu, paired)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

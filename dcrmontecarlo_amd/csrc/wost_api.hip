@@ -246,16 +246,16 @@ int upload_program(wost_handle* h) {
 // The field-specialised kernel for `mode` (with the walk recorder compiled in
 // when `record`), or nullptr when it is disabled or could not be built (the
 // precompiled kernel is used then; same results).
-hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1) {
+hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock) {
     if (!h->jit_enabled) return nullptr;
-    const int key = (2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns;
+    const int key = ((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 2 + (block != kWalkBlock ? 1 : 0);
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
     h->jit_mode = key;
     h->jit_version = h->prog_version;
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
                                          (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2),
-                                         record, ns);
+                                         record, ns, block);
     std::string err;
     hipFunction_t fn = nullptr;
     if (!jit_get_kernel(h->device, src, &fn, &err)) {
@@ -334,6 +334,32 @@ float silhouette_stop2(float rmin) {
     while (x > 0.0f && std::sqrt(x) > rmin) x = std::nextafter(x, 0.0f);
     while (std::sqrt(std::nextafter(x, INFINITY)) <= rmin) x = std::nextafter(x, INFINITY);
     return x;
+}
+
+// LDS staging of the segment tree's top levels (wost_walk.h, SegTree::lds): with
+// WOST_TREE_LDS=<records> (> 0) the field-specialised tree kernels run 896-thread
+// workgroups, two per CU (7 waves per SIMD, as the register budget allows), each
+// staging up to <records> records (whole levels, at most half the CU's 160 KiB of
+// LDS). Off by default: on C5 it measured slower than reading the records through
+// L1/L2 with 256-thread workgroups (4.09e9 with 511 records, 3.94e9 with 127, vs
+// 4.74e9 walk-steps/s; profiles/r02_tree/ab_tree_lds.log) -- the top levels stay
+// L1-resident anyway and the generic (flat) loads that serve both address spaces
+// cost more than the global ones.
+constexpr int kTreeBlock = 896;
+constexpr size_t kTreeLdsBudget = 80 * 1024;
+
+int tree_lds_records(const wost_handle* h, int mode, int n_points, int* block) {
+    *block = kWalkBlock;
+    const char* e = std::getenv("WOST_TREE_LDS");
+    if (!mode_tree(mode) || !e) return 0;
+    const int nd = (int)(h->dverts.size() / 2), nn = (int)(h->nverts.size() / 2);
+    const size_t base = walk_lds_bytes(mode, nd, nn, n_points, 0);
+    int n = base < kTreeLdsBudget ? (int)((kTreeLdsBudget - base) / (4 * sizeof(float4))) : 0;
+    n = std::min(std::min(n, h->tree.first_leaf), std::max(0, std::atoi(e)));
+    int full = 0;                      // whole levels only
+    while (2 * full + 1 <= n) full = 2 * full + 1;
+    if (full > 0) *block = kTreeBlock;
+    return full;
 }
 
 bool use_tree(const wost_handle* h) {
@@ -697,14 +723,21 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     } rec_free{d_rec};
     if (records) HIP_TRY(hipMalloc(&d_rec, (size_t)std::min<int64_t>(walks_total, batch_limit) * rec_walk_bytes));
 
-    const hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns);
+    int block = kWalkBlock;
+    int tree_lds = h->jit_enabled ? tree_lds_records(h, mode, (int)std::min<int64_t>(n_points, INT32_MAX), &block) : 0;
+    hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block);
+    if (!jfn && block != kWalkBlock) {   // the precompiled kernels run 256-thread workgroups, no staged tree
+        block = kWalkBlock;
+        tree_lds = 0;
+    }
     if (ns > 1 && !jfn)
         return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
                     h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
-    const size_t lds = walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points);
+    const size_t lds = walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
+                                      tree_lds);
     int blocks_per_cu = 0;
     if (jfn)
-        HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, kWalkBlock, lds));
+        HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
     else
         HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
                                &blocks_per_cu));
@@ -738,6 +771,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_leaf = h->tree.leaf;
         a.tree_tol = h->tree.tol;
         a.tree_stop2 = silhouette_stop2(a.rmin);
+        a.tree_lds_records = tree_lds;
     }
 
     std::vector<int64_t> begins;
@@ -770,16 +804,16 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.wid_begin = wb;
         a.count = count;
         const int64_t max_grid = (int64_t)blocks_per_cu * h->num_cus;
-        const int64_t want = (count + kWalkBlock - 1) / kWalkBlock;
+        const int64_t want = (count + block - 1) / block;
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
-        const int64_t waves = (int64_t)grid * (kWalkBlock / 64);
+        const int64_t waves = (int64_t)grid * (block / 64);
         a.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(1024, count / (waves * 4)));
         h->timing.grid_blocks = grid;
 
         HIP_TRY(hipEventRecord(h->ev[0], h->stream));
         if (jfn) {
             void* args[] = {&a};
-            HIP_TRY(hipModuleLaunchKernel(jfn, grid, 1, 1, kWalkBlock, 1, 1, (unsigned)lds, h->stream, args, nullptr));
+            HIP_TRY(hipModuleLaunchKernel(jfn, grid, 1, 1, block, 1, 1, (unsigned)lds, h->stream, args, nullptr));
         } else {
             HIP_TRY(launch_walk(mode, a, grid, h->stream));
         }

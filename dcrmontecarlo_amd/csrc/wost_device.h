@@ -927,9 +927,28 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     const float T = (dd * dd) * 1.002f;
     int k = 0, depth = 0;
     uint32_t pend = 0u, far_right = 0u;   // per level: second child pending / it is the right one
-    for (;;) {
-        bool climb = true;
-        if (k < t.first_leaf) {
+    // resume the deepest pending second child, re-tested against the tightened bound;
+    // false when nothing is pending (the search is over)
+    auto resume = [&]() {
+        while (pend != 0u) {
+            const int p = highest_bit(pend);
+            pend &= ~(1u << p);
+            const int anc = ((k + 1) >> (depth - p)) - 1;
+            const int side = (int)((far_right >> p) & 1u);
+            const float4* r = t.record(anc);
+            const float4 b = r[side], c = r[2 + side];
+            const float bound = best < T ? best : T;
+            k = 2 * anc + 1 + side;
+            depth = p + 1;
+            if (silhouette_keep(b, c, box_lower_bound2(b, px, py), bound, px, py)) return true;
+        }
+        return false;
+    };
+    // while-while (Aila & Laine): a lane that reaches a leaf waits until the wave's
+    // other lanes have also left the internal nodes, then the leaves are scanned together
+    bool live = true;
+    while (live) {
+        while (live && k < t.first_leaf) {
             WOST_TREE_COUNT(0);
             const float4* r = t.record(k);
             const float4 bl = r[0], br = r[1], cl = r[2], cr = r[3];
@@ -946,45 +965,32 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
                 }
                 k = 2 * k + 1 + (near_right ? 1 : 0);
                 ++depth;
-                climb = false;
+            } else {
+                live = resume();
             }
-        } else {
-            WOST_TREE_COUNT(1);
-            const int s0 = (k - t.first_leaf) * t.leaf;
-            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
-            const int j1 = s1 < nv - 2 ? s1 : nv - 2;
-            if (s0 + 1 <= j1) {
-                float2 va = t.v[s0], vb = t.v[s0 + 1];
-                for (int j = s0 + 1; j <= j1; ++j) {
-                    const float2 vc = t.v[j + 1];
-                    if (is_silhouette(va, vb, vc, px, py)) {
-                        const float ex = vb.x - px, ey = vb.y - py;
-                        const float d2 = ex * ex + ey * ey;
-                        best = d2 < best ? d2 : best;
-                    }
-                    va = vb;
-                    vb = vc;
+        }
+        if (!live) break;
+        WOST_TREE_COUNT(1);
+        const int s0 = (k - t.first_leaf) * t.leaf;
+        const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+        const int j1 = s1 < nv - 2 ? s1 : nv - 2;
+        if (s0 + 1 <= j1) {
+            float2 va = t.v[s0], vb = t.v[s0 + 1];
+            for (int j = s0 + 1; j <= j1; ++j) {
+                const float2 vc = t.v[j + 1];
+                if (is_silhouette(va, vb, vc, px, py)) {
+                    const float ex = vb.x - px, ey = vb.y - py;
+                    const float d2 = ex * ex + ey * ey;
+                    best = d2 < best ? d2 : best;
                 }
-                if (best <= stop2) return sqrtf(best);
+                va = vb;
+                vb = vc;
             }
+            if (best <= stop2) break;
         }
-        if (!climb) continue;
-        // resume the deepest pending second child, re-tested against the tightened bound
-        bool resumed = false;
-        while (pend != 0u) {
-            const int p = highest_bit(pend);
-            pend &= ~(1u << p);
-            const int anc = ((k + 1) >> (depth - p)) - 1;
-            const int side = (int)((far_right >> p) & 1u);
-            const float4* r = t.record(anc);
-            const float4 b = r[side], c = r[2 + side];
-            const float bound = best < T ? best : T;
-            k = 2 * anc + 1 + side;
-            depth = p + 1;
-            if (silhouette_keep(b, c, box_lower_bound2(b, px, py), bound, px, py)) { resumed = true; break; }
-        }
-        if (!resumed) return best == WOST_INF ? best : sqrtf(best);
+        live = resume();
     }
+    return best == WOST_INF ? best : sqrtf(best);
 }
 
 // intersect_polylines over the tree: the same winner as the full scan.
@@ -1011,9 +1017,18 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
     };
     int k = 0, depth = 0;
     uint32_t pend = 0u;   // per level: the right child is pending
-    for (;;) {
-        bool climb = true;
-        if (k < t.first_leaf) {
+    // the right child of the deepest pending level; false when nothing is pending
+    auto resume = [&]() {
+        if (pend == 0u) return false;
+        const int p = highest_bit(pend);
+        pend &= ~(1u << p);
+        k = 2 * (((k + 1) >> (depth - p)) - 1) + 2;
+        depth = p + 1;
+        return true;
+    };
+    bool live = true;
+    while (live) {                       // while-while, as in silhouette_distance_tree
+        while (live && k < t.first_leaf) {
             WOST_TREE_COUNT(2);
             const float4* rr = t.record(k);
             const bool okl = line_keep(rr[0]), okr = line_keep(rr[1]);
@@ -1021,28 +1036,24 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
                 if (okl && okr) pend |= 1u << depth;
                 k = 2 * k + (okl ? 1 : 2);   // left first: leaves in ascending segment order
                 ++depth;
-                climb = false;
-            }
-        } else {
-            WOST_TREE_COUNT(3);
-            const int s0 = (k - t.first_leaf) * t.leaf;
-            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
-            if (s0 < s1) {
-                float2 a = t.v[s0];
-                for (int i = s0; i < s1; ++i) {
-                    const float2 b = t.v[i + 1];
-                    const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
-                    if (s < best) { best = s; bi = i; }
-                    a = b;
-                }
+            } else {
+                live = resume();
             }
         }
-        if (!climb) continue;
-        if (pend == 0u) break;
-        const int p = highest_bit(pend);
-        pend &= ~(1u << p);
-        k = 2 * (((k + 1) >> (depth - p)) - 1) + 2;   // the right child of the depth-p ancestor
-        depth = p + 1;
+        if (!live) break;
+        WOST_TREE_COUNT(3);
+        const int s0 = (k - t.first_leaf) * t.leaf;
+        const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+        if (s0 < s1) {
+            float2 a = t.v[s0];
+            for (int i = s0; i < s1; ++i) {
+                const float2 b = t.v[i + 1];
+                const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
+                if (s < best) { best = s; bi = i; }
+                a = b;
+            }
+        }
+        live = resume();
     }
     return intersect_finish<NORMAL>(t.v, bi, best, px, py, dx, dy, qx, qy, r);
 }

@@ -257,7 +257,8 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
 }  // namespace
 
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
-                         const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources) {
+                         const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources,
+                         int block) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -343,7 +344,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    }\n};\n}  // namespace\n\n";
     int waves = 6;   // waves per SIMD the register budget is sized for (tools/ab_bench.sh)
     if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
-    o << "extern \"C\" __global__ void __launch_bounds__(wost::kWalkBlock, " << waves << ")\n"
+    o << "extern \"C\" __global__ void __launch_bounds__(" << block << ", " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
       << "    const GenFields fld{reinterpret_cast<const float*>(A.prog + "

@@ -27,9 +27,10 @@ constexpr int kJitMaxConstVertices = 40;
 // (Dirichlet dverts[2*nd], Neumann nverts[2*nn]) compiled in; `record`: the
 // kernel can record walks (return_history); `n_sources` > 1: the walk scores
 // sources SLOT_F, SLOT_EXTRA.. (multi-source batching).
+// `block`: threads per workgroup the kernel is launched with.
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record,
-                         int n_sources = 1);
+                         int n_sources = 1, int block = 256);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

@@ -48,6 +48,8 @@ struct WalkArgs {
     int32_t tree_leaf;
     float tree_tol;
     float tree_stop2;            // largest float whose sqrtf is <= rmin (< 0: none); silhouette_distance_tree
+    int32_t tree_lds_records;    // the first records of the tree staged in LDS (0: none)
+    int32_t pad_;
 };
 
 constexpr int kWalkBlock = 256;
@@ -66,13 +68,16 @@ WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
 // Bytes of dynamic LDS a walk-kernel workgroup needs. With the segment tree
 // the Neumann polyline stays in global memory (read through the caches).
+// With the segment tree, its first tree_lds records (64 B each) can be staged
+// too (they follow the query points).
 WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false,
-                                  bool delta = false) {
+                                  bool delta = false, int tree_lds = 0) {
     size_t b = align16(sizeof(float2) * (size_t)nd);
     if (neu && !tree) b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
     if (src) b += sizeof(float) * (size_t)kSamplerFloatsPadded;
     if (delta) b += sizeof(float4) * (size_t)kGnormCells;
     if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
+    if (tree) b += 4 * sizeof(float4) * (size_t)tree_lds;
     return b;
 }
 
@@ -115,13 +120,18 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     float4* sG = reinterpret_cast<float4*>(sT + (SRC ? kSamplerFloatsPadded : 0));   // G_norm cells
     float2* sP = reinterpret_cast<float2*>(sG + (DELTA ? kGnormCells : 0));
     const bool points_in_lds = A.n_points <= kLdsPointsMax;
+    float4* sTree = reinterpret_cast<float4*>(reinterpret_cast<unsigned char*>(sP) +
+                                              (points_in_lds ? align16(sizeof(float2) * (size_t)A.n_points) : 0));
 
     for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
     if (NEU && !TREE) {
         for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
         for (int i = threadIdx.x; i < A.nn - 1; i += blockDim.x) sPhi[i] = A.seg_phi[i];
     }
-    const SegTree tree{A.tree, nullptr, 0, A.nverts, A.nn, A.tree_first_leaf, A.tree_leaf, A.tree_tol};
+    if (TREE)   // the top levels of the segment tree (wost_device.h SegTree, child records)
+        for (int i = threadIdx.x; i < 4 * A.tree_lds_records; i += blockDim.x) sTree[i] = A.tree[i];
+    const SegTree tree{A.tree, TREE ? sTree : nullptr, TREE ? A.tree_lds_records : 0, A.nverts, A.nn,
+                       A.tree_first_leaf, A.tree_leaf, A.tree_tol};
     if (SRC)
         for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
     if (DELTA) {

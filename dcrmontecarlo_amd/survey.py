@@ -122,7 +122,38 @@ def paired_apparent_resistivity(model_walks: np.ndarray, bg_walks: np.ndarray, p
         R = A / B
         var = (vA - 2.0 * R * cAB + R * R * vB) / (B * B)
     rho = rho_bg * R
-    return ApparentResistivity(rho, rho_bg * np.sqrt(np.maximum(var, 0.0)), np.abs(B) > 3.0 * np.sqrt(vB))
+    se = rho_bg * np.sqrt(np.maximum(var, 0.0))
+    # the ratio is resolved when B != 0 and its own delta-method error is below a third of it
+    return ApparentResistivity(rho, se, (B != 0) & np.isfinite(rho) & (se <= np.abs(rho) / 3.0))
+
+
+def replica_rho_a(model_walks: np.ndarray, bg_walks: np.ndarray, pairs: np.ndarray, rho_bg: float,
+                  walks_per_replica: int) -> np.ndarray:
+    """rho_a of independent replicas of walks_per_replica paired walks each: [R, P] with
+    R = W // walks_per_replica (consecutive walks of every electrode form a replica)."""
+    m = np.asarray(model_walks, np.float64)
+    h = np.asarray(bg_walks, np.float64)
+    R = m.shape[1] // walks_per_replica
+    mm = m[:, :R * walks_per_replica].reshape(m.shape[0], R, walks_per_replica).mean(2)
+    hm = h[:, :R * walks_per_replica].reshape(h.shape[0], R, walks_per_replica).mean(2)
+    i, j = pairs[:, 0], pairs[:, 1]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return (rho_bg * (mm[i] - mm[j]) / (hm[i] - hm[j])).T
+
+
+def matched_walk_pvalues(replicas: np.ndarray, observed: np.ndarray) -> np.ndarray:
+    """Two-sided mid-p value of each observed rho_a among the replicas' values of the
+    same dipole (non-finite replicas ignored): is the observation a plausible draw of
+    the replicated estimator at the same walk count?"""
+    out = np.full(len(observed), np.nan)
+    for d in range(len(observed)):
+        r = replicas[:, d]
+        r = r[np.isfinite(r)]
+        if len(r) == 0 or not np.isfinite(observed[d]):
+            continue
+        lt, eq = np.mean(r < observed[d]), np.mean(r == observed[d])
+        out[d] = min(1.0, 2.0 * min(lt + 0.5 * eq, 1.0 - lt - 0.5 * eq))
+    return out
 
 
 @dataclass

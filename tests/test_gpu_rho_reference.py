@@ -1,0 +1,77 @@
+"""The C4 DCR survey against the reference's own run (BASELINE.json metric, part 2).
+
+tests/golden/rho_dcr_dipole.npz holds the reference's per-walk values at all 48
+C4 electrodes (tools/gen_fixtures.py --only rho: the reference's _solveUnified with
+its own torch/numpy RNG, 400 walks each, eps = 0.9, for the model conductivity
+tests/testGeophysicalScenario.py:35-55 and the homogeneous alpha = 100 background,
+on common random numbers). The device must reproduce it statistically:
+
+* potentials: each reference 400-walk electrode mean is a plausible 400-walk mean of
+  the device's walks (bootstrap, two-sided p > 1e-3 per electrode, both fields);
+* apparent resistivity: the reference's dipole-dipole rho_a (paired, 400 walks) is a
+  plausible draw of the device's rho_a at 400 walks (512 replicas; mid-p > 1e-3 for
+  every dipole), and the device's precise estimate lies within the spread of those
+  400-walk replicas.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+
+pytestmark = pytest.mark.gpu
+
+ALPHA_BG = 100.0
+
+
+def _paired(n_walks, seed=2024):
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd import survey
+
+    sc = S.dcr_dipole()
+    sm = sc.solver(device=0)
+    sh = survey.homogeneous_solver(sc, ALPHA_BG, sm, device=0)
+    assert sm.sigma_bar == sh.sigma_bar == 10.0          # the reference's Q8 fallback for both
+    vm, stm = sm.solve_walks(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=seed)
+    vh, sth = sh.solve_walks(sc.points, nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=seed)
+    return vm.astype(np.float64), vh.astype(np.float64), stm, sth
+
+
+def test_common_random_numbers_share_paths(gpu_available):
+    """Model and background walks of one seed take identical paths (same step counts),
+    as the reference's do (fixture flag common_paths, checked by the generator)."""
+    z = golden("rho_dcr_dipole.npz")
+    assert bool(z["common_paths"])
+    vm, vh, stm, sth = _paired(2048)
+    np.testing.assert_array_equal(stm, sth)
+
+
+def test_potentials_vs_reference_rng(gpu_available):
+    from test_oracle_golden import bootstrap_pvalues
+
+    z = golden("rho_dcr_dipole.npz")
+    n_ref = int(z["n_walks"])
+    vm, vh, _, _ = _paired(20000, seed=77)
+    for walks, ref in ((vm, z["model_values"]), (vh, z["background_values"])):
+        p = bootstrap_pvalues(walks, n_ref, ref.mean(1), n_boot=2000)
+        assert p.min() > 1e-3, p
+
+
+def test_apparent_resistivity_vs_reference(gpu_available):
+    from dcrmontecarlo_amd import survey
+
+    z = golden("rho_dcr_dipole.npz")
+    ref = survey.reference_rho_a(os.path.join(GOLDEN, "rho_dcr_dipole.npz"))
+    n_ref = ref.walks
+    vm, vh, _, _ = _paired(n_ref * 512)
+    pairs = survey.dipole_dipole_pairs(vm.shape[0])
+    rep = survey.replica_rho_a(vm, vh, pairs, 1.0 / ALPHA_BG, n_ref)
+    p = survey.matched_walk_pvalues(rep, ref.rho.rho_a)
+    assert np.all(np.isfinite(p)), p
+    assert p.min() > 1e-3, p
+    # the precise paired estimate sits inside the 400-walk replicas' central 99.8%
+    gpu = survey.paired_apparent_resistivity(vm, vh, pairs, 1.0 / ALPHA_BG)
+    lo, hi = np.nanquantile(rep, [0.001, 0.999], axis=0)
+    assert np.all((gpu.rho_a >= lo) & (gpu.rho_a <= hi))
+    assert int(z["n_walks"]) == n_ref
