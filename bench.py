@@ -137,9 +137,9 @@ def reference_leg(survey, alpha_bg, vm, vh):
         return None
     pairs = survey.dipole_dipole_pairs(vm.shape[0])
     gpu = survey.paired_apparent_resistivity(vm, vh, pairs, 1.0 / alpha_bg)
-    out = survey.compare_to_reference(gpu, ref)
-    out["gpu_walks_per_electrode"] = int(vm.shape[1])
     rep = survey.replica_rho_a(vm, vh, pairs, 1.0 / alpha_bg, ref.walks)
+    out = survey.compare_to_reference(gpu, ref, replicas=rep)
+    out["gpu_walks_per_electrode"] = int(vm.shape[1])
     p = survey.matched_walk_pvalues(rep, ref.rho.rho_a)
     ok = np.isfinite(p)
     out["matched_walks"] = {"replicas": int(rep.shape[0]), "walks_per_replica": int(ref.walks),

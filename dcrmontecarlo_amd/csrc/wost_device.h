@@ -176,6 +176,40 @@ WOST_HD float ipowf(float x, int n) {
     return r;
 }
 
+// ---- saturation shortcuts ----------------------------------------------------
+// A sharp sigmoid (torch_smooth_circle has k = -100) is exactly 0 or 1 in float32
+// a short distance from its circle, and an electrode Gaussian is exactly 0 a few
+// widths from its centre. When every lane of the wave is in such a region the
+// transcendentals are skipped and the exact results of the full expressions are
+// returned instead -- including the signed zeros of the derivatives and the NaN
+// that rsq(0) makes at a circle's centre -- so the values are bit for bit those
+// of the full path. Saturation, with z = k (d - R) and s = 1 / (1 + exp(-z)):
+//  * z <= -90: exp(-z) >= e^90 overflows to +inf (v_exp_f32 of 129.8), s = +0;
+//  * z >= 20:  0 < exp(-z) <= 2.1e-9 < 2^-25, 1 + exp(-z) rounds to 1, s = 1.
+// The distance thresholds carry a margin of 1e-3 (R + band) for the rounding of
+// d (v_sqrt / v_rsq, a few ulp). A Gaussian exp(q) with q < -110 is v_exp_f32 of
+// < -158, +0. WOST_NO_SATURATION_SHORTCUTS turns them off (bitwise A/B checks).
+struct RadialSat { float lo2, hi2, s_in, s_out; };
+WOST_HD RadialSat radial_saturation(float k, float R) {
+    RadialSat r{-1.0f, WOST_INF, 0.0f, 0.0f};
+    const float ak = fabsf(k);
+    if (!(ak > 0.0f) || !(ak < WOST_INF) || !(fabsf(R) < 1e30f)) return r;
+    const float out_band = (k < 0.0f ? 90.0f : 20.0f) / ak, in_band = (k < 0.0f ? 20.0f : 90.0f) / ak;
+    const float ho = R + out_band, hi_ = R - in_band;
+    const float m = 1e-3f * (fabsf(R) + out_band + in_band) + 1e-30f;
+    r.hi2 = (ho + m) * (ho + m);
+    r.lo2 = (hi_ - m > 0.0f) ? (hi_ - m) * (hi_ - m) : -1.0f;
+    r.s_out = k < 0.0f ? 0.0f : 1.0f;
+    r.s_in = k < 0.0f ? 1.0f : 0.0f;
+    return r;
+}
+#if defined(WOST_NO_SATURATION_SHORTCUTS)
+#define WOST_SAT_ALL(c) false
+#else
+#define WOST_SAT_ALL(c) (!WOST_ANY(!(c)))
+#endif
+constexpr float kExpZeroBelow = -110.0f;
+
 // ---- per-kind values ------------------------------------------------------
 WOST_HD float fv_mono(float x, float y, int a, int b) { return ipowf(x, a) * ipowf(y, b); }
 WOST_HD float fv_exp_quad(float x, float y, float cx, float cy, float axx, float ayy, float axy, float ax,
@@ -187,7 +221,9 @@ WOST_HD float fv_exp_quad(float x, float y, float cx, float cy, float axx, float
 // the dropped terms only add signed zeros, so the value is fv_exp_quad's.
 WOST_HD float fv_exp_quad_diag(float x, float y, float cx, float cy, float axx, float ayy) {
     float dx = x - cx, dy = y - cy;
-    return f_exp(axx * (dx * dx) + ayy * (dy * dy));
+    const float q = axx * (dx * dx) + ayy * (dy * dy);
+    if (WOST_SAT_ALL(q < kExpZeroBelow)) return 0.0f;
+    return f_exp(q);
 }
 WOST_HD bool exp_quad_is_diag(const float* p) { return p[4] == 0.f && p[5] == 0.f && p[6] == 0.f && p[7] == 0.f; }
 WOST_HD float fv_sin_lin(float x, float y, float a, float b, float c) { return f_sin(a * x + b * y + c); }
@@ -196,7 +232,11 @@ WOST_HD float fv_sigmoid_lin(float x, float y, float a, float b, float c) { retu
 // utils.py:128-129: sdf = ||x - c|| - R ; sigmoid(k * sdf)
 WOST_HD float fv_sigmoid_radial(float x, float y, float k, float cx, float cy, float R) {
     float dx = x - cx, dy = y - cy;
-    return sigmoidf(k * (f_sqrt(dx * dx + dy * dy) - R));
+    const float d2 = dx * dx + dy * dy;
+    const RadialSat sat = radial_saturation(k, R);
+    const bool out = d2 >= sat.hi2, in = d2 <= sat.lo2;
+    if (WOST_SAT_ALL(out || in)) return out ? sat.s_out : sat.s_in;
+    return sigmoidf(k * (f_sqrt(d2) - R));
 }
 WOST_HD float fv_ind_box(float x, float y, float x0, float x1, float y0, float y1) {
     return (x >= x0 && x <= x1 && y >= y0 && y <= y1) ? 1.0f : 0.0f;
@@ -231,7 +271,8 @@ WOST_HD Jet fj_exp_quad(float x, float y, float cx, float cy, float axx, float a
 }
 WOST_HD Jet fj_exp_quad_diag(float x, float y, float cx, float cy, float axx, float ayy) {
     float dx = x - cx, dy = y - cy;
-    float e = f_exp(axx * (dx * dx) + ayy * (dy * dy));
+    const float q = axx * (dx * dx) + ayy * (dy * dy);
+    float e = WOST_SAT_ALL(q < kExpZeroBelow) ? 0.0f : f_exp(q);
     float qx = 2.f * axx * dx;
     float qy = 2.f * ayy * dy;
     return Jet{e, e * qx, e * qy, e * (qx * qx + qy * qy + 2.f * (axx + ayy))};
@@ -252,9 +293,18 @@ WOST_HD Jet fj_sigmoid_lin(float x, float y, float a, float b, float c) {
 WOST_HD Jet fj_sigmoid_radial(float x, float y, float k, float cx, float cy, float R) {
     float dx = x - cx, dy = y - cy;
     float d2 = dx * dx + dy * dy;
-    float inv = f_rsq(d2);             // one transcendental for d and 1/d
-    float d = d2 > 0.f ? d2 * inv : 0.f;
-    float s = sigmoidf(k * (d - R));
+    const RadialSat sat = radial_saturation(k, R);
+    const bool out = d2 >= sat.hi2, in = d2 <= sat.lo2;
+    float inv, s;
+    if (WOST_SAT_ALL(out || in)) {
+        // s1 = s2 = 0: inv only carries its sign (+) and rsq(0) = +inf into the derivatives
+        inv = d2 > 0.f ? 1.0f : WOST_INF;
+        s = out ? sat.s_out : sat.s_in;
+    } else {
+        inv = f_rsq(d2);               // one transcendental for d and 1/d
+        float d = d2 > 0.f ? d2 * inv : 0.f;
+        s = sigmoidf(k * (d - R));
+    }
     float s1 = s * (1.f - s);          // ds/dz
     float s2 = s1 * (1.f - 2.f * s);   // d2s/dz2
     // z = k (d - R): grad z = k (x-c)/d, lap z = k/d (2-D), |grad z|^2 = k^2

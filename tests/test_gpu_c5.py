@@ -1,0 +1,118 @@
+"""C5 at its BASELINE configuration: the 10,000-segment topography (SURVEY 8d C5,
+notebook cells 17-18 fields and U boundary) with the 256-electrode line, walked
+through the segment tree, against the reference's brute-force scans restated by
+the CPU oracle (geometry/PolylinesSimple.py:25-49, :83-102, :134-197).
+
+* every step of recorded device walks: the Dirichlet distance and the Neumann
+  silhouette distance the tree kernel used equal the oracle's full scans bit for
+  bit (the tree must not change a single query);
+* device vs oracle on the same Philox streams (16 electrodes x 256 walks): a
+  chaos-aware walk-agreement floor -- the oracle against itself under a 1-ulp
+  direction perturbation agrees on 86.5% of these walks (their Q1 Neumann "hits"
+  make C5 the most chaotic scenario) -- and per-electrode means within 3
+  combined standard errors;
+* full size (256 electrodes x 10k walks): u(2f) = 2 u(f) bit for bit, and the tree
+  kernel equals the brute-force scan kernel walk for walk on a subset;
+* the Wenner survey's multi-source batching equals per-source solves bit for bit.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+AGREEMENT_FLOOR_C5 = 0.80
+
+
+def _c5(**kw):
+    from dcrmontecarlo_amd import scenarios as S
+
+    return S.wenner_topography(**kw)
+
+
+def test_c5_tree_queries_along_walks_match_full_scans(gpu_available):
+    from oracle import oracle as O
+
+    sc = _c5()
+    s = sc.solver(device=0)
+    pts = sc.points[4::32]
+    u, hist = s.solve(pts, nWalks=24, maxSteps=sc.max_steps, eps=sc.eps, seed=17, return_history=True)
+    assert s.last_timing["tree"] == 1
+    P, DD, DN = [], [], []
+    for i in range(len(pts)):
+        for w in hist[i]:
+            for st in w["path"]:
+                P.append(np.asarray(st["point"], np.float32))
+                DD.append(st["dirichlet_distance"])
+                DN.append(st["neumann_distance"])
+    P = np.array(P, np.float32)
+    DD, DN = np.array(DD, np.float32), np.array(DN, np.float32)
+    assert len(P) > 10000
+    dd_o = O.geometry("distance", sc.dirichlet, P)
+    dn_o = O.geometry("silhouetteDistance", sc.neumann, P)
+    np.testing.assert_array_equal(DD.view(np.uint32), dd_o.view(np.uint32))
+    np.testing.assert_array_equal(DN.view(np.uint32), dn_o.view(np.uint32))
+    assert np.isfinite(DN).sum() > 100          # silhouettes were found along the walks
+
+
+def test_c5_device_matches_oracle(gpu_available):
+    from oracle import oracle as O
+
+    sc = _c5()
+    s = sc.solver(device=0)
+    pts = sc.points[8::16][:16]
+    W = 256
+    gv, gs = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=31337)
+    gv, gs = gv.ravel(), gs.ravel()
+    ov, os_ = O.Problem.from_scenario(sc, sigma_bar=s.sigma_bar).solve_walks(pts, W, sc.max_steps, sc.eps, 31337)
+    scale = max(float(np.abs(ov).max()), 1e-30)
+    same = (gs == os_) & (np.abs(gv - ov) <= 1e-3 * np.abs(ov) + 1e-5 * scale)
+    assert same.mean() >= AGREEMENT_FLOOR_C5, same.mean()
+    g = gv.astype(np.float64).reshape(len(pts), W)
+    o = ov.astype(np.float64).reshape(len(pts), W)
+    se = np.sqrt(g.var(1, ddof=1) / W + o.var(1, ddof=1) / W)
+    assert np.all(np.abs(g.mean(1) - o.mean(1)) <= 3.0 * se + 1e-9 * scale)
+
+
+def test_c5_full_size_linearity_and_tree_equals_scan(gpu_available):
+    from dcrmontecarlo_amd.geometry import PolyLinesSimple
+    from dcrmontecarlo_amd.solvers import WostSolver_2D
+
+    sc = _c5(n_electrodes=256, n_walks=10_000)
+    mk = lambda f: WostSolver_2D(PolyLinesSimple(sc.dirichlet), sc.g, PolyLinesSimple(sc.neumann), source=f,
+                                 alpha=sc.alpha)
+    s1, s2 = mk(sc.f), mk(2.0 * sc.f)
+    u1, st1 = s1.solve(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=21, return_stats=True)
+    assert s1.last_timing["tree"] == 1
+    u2, st2 = s2.solve(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=21, return_stats=True)
+    assert np.all(np.isfinite(st1.mean))
+    assert np.array_equal(st2.mean, 2.0 * st1.mean)
+    assert st1.total_steps == st2.total_steps > 256 * 10_000 * 50
+    # the tree kernel against the brute-force scan kernel, walk for walk, on a subset
+    sub = sc.points[::32]
+    tv, ts = s1.solve_walks(sub, nWalks=64, maxSteps=sc.max_steps, eps=sc.eps, seed=23)
+    s1.set_segment_tree(-1)
+    bv, bs = s1.solve_walks(sub, nWalks=64, maxSteps=sc.max_steps, eps=sc.eps, seed=23)
+    assert s1.last_timing["tree"] == 0
+    np.testing.assert_array_equal(ts, bs)
+    np.testing.assert_array_equal(tv.view(np.uint32), bv.view(np.uint32))
+
+
+def test_c5_wenner_survey_batches_equal_single_source_solves(gpu_available):
+    from dcrmontecarlo_amd import survey
+
+    sc = _c5(n_electrodes=40, n_walks=256)
+    res = survey.run_wenner_survey(sc, 1e-2, n_walks=256, seed=3)
+    Q = len(res.quadripoles)
+    assert Q == 37 and res.launches == len(list(survey.wenner_batches(40, 1)))
+    assert np.all(np.isfinite(res.model.dv)) and np.all(np.isfinite(res.background.dv))
+    # quadripole q from a single-source solve of its own transmitter, same group seed
+    sm = sc.solver(device=0)
+    for g, (j0, j1, t0, t1) in enumerate(survey.wenner_batches(40, 1)):
+        gseed = (3 * 0x9E3779B1 + g) & (2**64 - 1)
+        for q in (t0, t1 - 1):
+            if not (j0 <= q + 1 < j1 and j0 <= q + 2 < j1):
+                continue
+            sm.setSourceTerm(survey.dipole_source(sc.points[q], sc.points[q + 3], 0.5))
+            u, st = sm.solve(sc.points[j0:j1], nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=gseed,
+                             return_stats=True)
+            assert st.mean[q + 1 - j0] - st.mean[q + 2 - j0] == res.model.dv[q]

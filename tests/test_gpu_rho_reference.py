@@ -10,8 +10,8 @@ on common random numbers). The device must reproduce it statistically:
   the device's walks (bootstrap, two-sided p > 1e-3 per electrode, both fields);
 * apparent resistivity: the reference's dipole-dipole rho_a (paired, 400 walks) is a
   plausible draw of the device's rho_a at 400 walks (512 replicas; mid-p > 1e-3 for
-  every dipole), and the device's precise estimate lies within the spread of those
-  400-walk replicas.
+  every dipole), and the RMSE of the device's precise estimate against the reference
+  is within the 1-sigma error of a 400-walk estimate (north star).
 """
 import os
 
@@ -70,8 +70,13 @@ def test_apparent_resistivity_vs_reference(gpu_available):
     p = survey.matched_walk_pvalues(rep, ref.rho.rho_a)
     assert np.all(np.isfinite(p)), p
     assert p.min() > 1e-3, p
-    # the precise paired estimate sits inside the 400-walk replicas' central 99.8%
+    # the north-star form: the precise device estimate's RMSE against the reference's
+    # rho_a is within the 1-sigma Monte-Carlo error of a 400-walk estimate (the spread of
+    # the 512 replicas; the reference's own delta-method error from 400 heavy-tailed walks
+    # understates it by orders of magnitude), over the dipoles it resolves
     gpu = survey.paired_apparent_resistivity(vm, vh, pairs, 1.0 / ALPHA_BG)
-    lo, hi = np.nanquantile(rep, [0.001, 0.999], axis=0)
-    assert np.all((gpu.rho_a >= lo) & (gpu.rho_a <= hi))
+    cmp = survey.compare_to_reference(gpu, ref, replicas=rep)
+    assert cmp["resolved"] >= 20, cmp
+    assert cmp["rmse"] <= cmp["replica_1sigma_rms"], cmp
+    assert cmp["z_rms"] < 1.5 and cmp["z_max"] < 4.0, cmp
     assert int(z["n_walks"]) == n_ref

@@ -23,6 +23,42 @@ def test_wenner_quadripoles():
     assert survey.wenner_quadripoles(3, a=1).shape == (0, 4)
 
 
+@pytest.mark.parametrize("E,a", [(256, 1), (256, 5), (40, 1), (7, 2), (16, 1)])
+def test_wenner_batches_walk_each_receiver_once(E, a):
+    """Multi-source batching of a Wenner line: each of a quadripole's receivers M and N is
+    solved in a group holding its transmitter, at most 16 transmitters per group, and
+    every electrode belongs to one group (walked once per field)."""
+    groups = list(survey.wenner_batches(E, a))
+    seen = []
+    for j0, j1, t0, t1 in groups:
+        assert 0 < t1 - t0 <= 16 and 0 <= j0 < j1 <= E
+        seen.extend(range(j0, j1))
+    assert len(seen) == len(set(seen))
+    for q, (A, M, N, B) in enumerate(survey.wenner_quadripoles(E, a)):
+        for e in (M, N):
+            assert any(j0 <= e < j1 and t0 <= q < t1 for j0, j1, t0, t1 in groups), (q, e)
+
+
+def test_paired_rho_a_and_replicas():
+    """Common random numbers: identical model and background walks give rho_bg with a zero
+    error; the replicas and matched-walk p-values behave on known inputs."""
+    rng = np.random.default_rng(0)
+    h = rng.exponential(size=(4, 800)) * np.array([[4.0], [3.0], [2.0], [1.0]])
+    pairs = survey.dipole_dipole_pairs(4)
+    r = survey.paired_apparent_resistivity(h, h, pairs, 0.01)
+    np.testing.assert_allclose(r.rho_a, 0.01)
+    np.testing.assert_allclose(r.se, 0.0, atol=1e-9)
+    assert r.resolved.all()
+    m = 2.0 * h                                        # a uniformly doubled response: rho_a = 2 rho_bg
+    r2 = survey.paired_apparent_resistivity(m, h, pairs, 0.01)
+    np.testing.assert_allclose(r2.rho_a, 0.02)
+    rep = survey.replica_rho_a(m, h, pairs, 0.01, 100)
+    assert rep.shape == (8, 3)
+    np.testing.assert_allclose(rep, 0.02)
+    p = survey.matched_walk_pvalues(rep, np.array([0.02, 0.03, 0.01]))
+    assert p.tolist() == [1.0, 0.0, 0.0]
+
+
 def test_potential_differences_and_errors():
     u = np.array([3.0, 1.0, 0.5])
     se = np.array([0.3, 0.4, 0.0])
