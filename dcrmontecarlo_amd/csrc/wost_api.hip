@@ -253,9 +253,16 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
     h->jit_fn = nullptr;
     h->jit_mode = key;
     h->jit_version = h->prog_version;
+    const int nn = (int)(h->nverts.size() / 2);
+    std::vector<float> phi;   // a compiled-in Neumann polyline carries the device's segment angles
+    if (jit_const_neumann(mode, nn) && nn >= 2) {
+        phi.resize(nn - 1);
+        if (hipMemcpy(phi.data(), h->d_seg_phi, sizeof(float) * phi.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return nullptr;
+    }
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
-                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2),
-                                         record, ns, block);
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), nn, record, ns, block,
+                                         phi.empty() ? nullptr : phi.data());
     std::string err;
     hipFunction_t fn = nullptr;
     if (!jit_get_kernel(h->device, src, &fn, &err)) {
@@ -733,8 +740,9 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if (ns > 1 && !jfn)
         return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
                     h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
-    const size_t lds = walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
-                                      tree_lds);
+    const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
+    const size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(nd_),
+                                      jfn && jit_const_neumann(mode, nn_));
     int blocks_per_cu = 0;
     if (jfn)
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
@@ -743,7 +751,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
                                &blocks_per_cu));
     if (blocks_per_cu < 1)
         return fail(WOST_ERR_UNSUPPORTED, "walk kernel does not fit on a CU (polylines too large for LDS: %zu bytes)",
-                    walk_lds_bytes(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points));
+                    lds);
 
     WalkArgs a{};
     a.points = h->d_points;
@@ -927,9 +935,18 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
     if (rc != WOST_OK) return rc;
     build_program(h->fields, h->sigma_bar, h->prog);
     const int mode = walk_mode(h);
+    // no device here: the segment angles of a compiled-in Neumann polyline come from the
+    // host's atan2f (the kernels use the device's bits; this source is for offline study)
+    const int nn = (int)(h->nverts.size() / 2);
+    std::vector<float> phi(nn > 1 ? nn - 1 : 0);
+    for (int i = 0; i + 1 < nn; ++i) {
+        const float2 a{h->nverts[2 * i], h->nverts[2 * i + 1]}, b{h->nverts[2 * i + 2], h->nverts[2 * i + 3]};
+        const float2 n = segment_left_normal(a, b);
+        phi[i] = std::atan2(n.y, n.x);
+    }
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
-                                         (int)(h->dverts.size() / 2), h->nverts.data(), (int)(h->nverts.size() / 2),
-                                         false);
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), nn, false, 1, kWalkBlock,
+                                         phi.empty() ? nullptr : phi.data());
     delete h;
     *length = (int64_t)src.size();
     if (out && capacity > 0) {

@@ -27,8 +27,13 @@
 // header tests the lane's own condition)
 #if defined(__HIP_DEVICE_COMPILE__)
 #define WOST_ANY(c) __any(c)
+// Keeps a wave-uniform branch a branch: without it the compiler may evaluate a short
+// guarded expression (an exp, a square root) for every lane and select the result,
+// which costs the transcendental issue slots the guard is there to save.
+#define WOST_NO_SPECULATION() __asm__ volatile("" ::: "memory")
 #else
 #define WOST_ANY(c) (c)
+#define WOST_NO_SPECULATION() ((void)0)
 #endif
 
 namespace wost {
@@ -222,8 +227,12 @@ WOST_HD float fv_exp_quad(float x, float y, float cx, float cy, float axx, float
 WOST_HD float fv_exp_quad_diag(float x, float y, float cx, float cy, float axx, float ayy) {
     float dx = x - cx, dy = y - cy;
     const float q = axx * (dx * dx) + ayy * (dy * dy);
-    if (WOST_SAT_ALL(q < kExpZeroBelow)) return 0.0f;
-    return f_exp(q);
+    float e = 0.0f;
+    if (!WOST_SAT_ALL(q < kExpZeroBelow)) {
+        WOST_NO_SPECULATION();
+        e = f_exp(q);
+    }
+    return e;
 }
 WOST_HD bool exp_quad_is_diag(const float* p) { return p[4] == 0.f && p[5] == 0.f && p[6] == 0.f && p[7] == 0.f; }
 WOST_HD float fv_sin_lin(float x, float y, float a, float b, float c) { return f_sin(a * x + b * y + c); }
@@ -272,7 +281,11 @@ WOST_HD Jet fj_exp_quad(float x, float y, float cx, float cy, float axx, float a
 WOST_HD Jet fj_exp_quad_diag(float x, float y, float cx, float cy, float axx, float ayy) {
     float dx = x - cx, dy = y - cy;
     const float q = axx * (dx * dx) + ayy * (dy * dy);
-    float e = WOST_SAT_ALL(q < kExpZeroBelow) ? 0.0f : f_exp(q);
+    float e = 0.0f;
+    if (!WOST_SAT_ALL(q < kExpZeroBelow)) {
+        WOST_NO_SPECULATION();
+        e = f_exp(q);
+    }
     float qx = 2.f * axx * dx;
     float qy = 2.f * ayy * dy;
     return Jet{e, e * qx, e * qy, e * (qx * qx + qy * qy + 2.f * (axx + ayy))};
@@ -500,6 +513,7 @@ constexpr int kGnormCells = 256;
 constexpr float kGnormInvH = 12.0f;
 constexpr float kGnormXMax = (float)kGnormCells / kGnormInvH;
 constexpr int kSamplerFloatsPadded = (WOST_SAMPLER_TABLE_N + 3) & ~3;   // gnorm cells follow, 16-byte aligned
+constexpr int kSamplerTailFloats = WOST_SAMPLER_TABLE_N - 1;              // LDS copy: nodes 1..N-1
 
 template <class TabP>
 WOST_HD float greens_norm_from_table(TabP cells, float x, float r, float inv_sb) {
@@ -528,6 +542,22 @@ WOST_HD float sample_rho(TabP tab, float u) {
     if (i > WOST_SAMPLER_TABLE_N - 2) i = WOST_SAMPLER_TABLE_N - 2;
     float f = pos - (float)i;
     float a = tab[i], b = tab[i + 1];
+    return a + f * (b - a);
+}
+
+// The same with the walk kernels' LDS copy of the table: tail = nodes 1..N-1 (the
+// word before tail is readable LDS) and node 0 in a register, so that the pair
+// (node i, node i+1) is one ds_read2_b32 at tail + i - 1 and the copy is 4 bytes
+// shorter (20,480 bytes of LDS with the G_norm cells: 8 workgroups per CU).
+WOST_HD float sample_rho_tail(const float* tail, float node0, float u) {
+#pragma clang fp contract(off)
+    float pos = u * (float)(WOST_SAMPLER_TABLE_N - 1);
+    int i = (int)pos;
+    if (i > WOST_SAMPLER_TABLE_N - 2) i = WOST_SAMPLER_TABLE_N - 2;
+    float f = pos - (float)i;
+    const float* q = tail + (i - 1);
+    float a = q[0], b = q[1];
+    a = i == 0 ? node0 : a;
     return a + f * (b - a);
 }
 

@@ -41,9 +41,12 @@ inline bool mode_src(int m) {
 }
 inline bool mode_delta(int m) { return m == MODE_DELTA || m == MODE_MIXED_DELTA || m == MODE_MIXED_DELTA_TREE; }
 
-inline size_t walk_lds_bytes(int mode, int nd, int nn, int n_points, int tree_lds = 0) {
+// const_d / const_n: the kernel has the Dirichlet / Neumann polyline compiled in
+// (field-specialised kernels, wost_jit.cpp), so it stages no copy.
+inline size_t walk_lds_bytes(int mode, int nd, int nn, int n_points, int tree_lds = 0, bool const_d = false,
+                             bool const_n = false) {
     return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points, mode_tree(mode), mode_delta(mode),
-                              tree_lds);
+                              tree_lds, const_d, const_n && !mode_fix(mode));
 }
 // floats of the sampler / G_norm table buffer (WalkArgs::table)
 inline size_t table_floats(bool delta) {

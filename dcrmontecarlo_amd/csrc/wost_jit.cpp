@@ -256,9 +256,21 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
 
 }  // namespace
 
+int jit_const_vertices() {
+    int max_const = kJitMaxConstVertices;   // A/B knob: WOST_JIT_CONST_VERTICES (an integer)
+    if (const char* e = std::getenv("WOST_JIT_CONST_VERTICES")) max_const = std::max(0, std::min(256, std::atoi(e)));
+    return max_const;
+}
+
+bool jit_const_dirichlet(int nd) { return nd <= jit_const_vertices(); }
+
+bool jit_const_neumann(int mode, int nn) {
+    return mode_neu(mode) && !mode_tree(mode) && nn >= 1 && nn <= jit_const_vertices();
+}
+
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources,
-                         int block) {
+                         int block, const float* seg_phi) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -299,10 +311,13 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    __device__ __forceinline__ float inv_sigma_bar() const { return " << lit(hdr.inv_sigma_bar) << "; }\n";
     // a short Dirichlet polyline is compiled in: the scan unrolls, the segment
     // vectors and squared lengths fold to constants (the same IEEE operations)
+    const bool dconst = jit_const_dirichlet(nd);
+    // a compiled-in Neumann polyline also needs its segment angles as constants
+    const bool nconst = jit_const_neumann(mode, nn) && (seg_phi != nullptr || nn < 2);
+    o << "    static constexpr bool kConstDirichlet = " << (dconst ? "true" : "false") << ";\n";
+    o << "    static constexpr bool kConstNeumann = " << (nconst ? "true" : "false") << ";\n";
     o << "    __device__ __forceinline__ float dirichlet_distance(const float2* sD, int nd, float x, float y) const {\n";
-    int max_const = kJitMaxConstVertices;   // A/B knob: WOST_JIT_CONST_VERTICES (an integer)
-    if (const char* e = std::getenv("WOST_JIT_CONST_VERTICES")) max_const = std::max(0, std::min(256, std::atoi(e)));
-    if (nd <= max_const) {
+    if (dconst) {
         o << "        const float2 v[" << nd << "] = {";
         for (int i = 0; i < nd; ++i) o << (i ? ", " : "") << "{" << lit(dverts[2 * i]) << ", " << lit(dverts[2 * i + 1]) << "}";
         o << "};\n";
@@ -325,7 +340,6 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "        return wost::poly_distance(sD, nd, x, y);\n";
     }
     o << "    }\n";
-    const bool nconst = neu && !tree && nn >= 1 && nn <= max_const;
     auto nverts_decl = [&]() {
         std::ostringstream v;
         v << "        const float2 v[" << nn << "] = {";
@@ -341,6 +355,15 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
          " float dy, float r) const {\n";
     if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
     else o << "        return wost::intersect_polylines<false>(sN, nn, x, y, dx, dy, r);\n";
+    o << "    }\n";
+    o << "    __device__ __forceinline__ float neumann_phi(const float* sPhi, int seg) const {\n";
+    if (nconst && nn >= 2) {
+        o << "        const float phi[" << nn - 1 << "] = {";
+        for (int i = 0; i + 1 < nn; ++i) o << (i ? ", " : "") << lit(seg_phi[i]);
+        o << "};\n        return phi[seg];\n";
+    } else {
+        o << "        return sPhi[seg];\n";
+    }
     o << "    }\n};\n}  // namespace\n\n";
     int waves = 6;   // waves per SIMD the register budget is sized for (tools/ab_bench.sh)
     if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));

@@ -19,18 +19,25 @@
 namespace wost {
 
 // Polylines of at most this many vertices are compiled into the specialised
-// kernel as constants.
+// kernel as constants (and then not staged in LDS).
 constexpr int kJitMaxConstVertices = 40;
+// The threshold in force: kJitMaxConstVertices, or WOST_JIT_CONST_VERTICES (A/B knob).
+int jit_const_vertices();
+// Which polylines a specialised kernel of `mode` compiles in.
+bool jit_const_dirichlet(int nd);
+bool jit_const_neumann(int mode, int nn);
 
 // HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
 // (wost_internal.h WalkMode) with the fields of `prog` and short polylines
 // (Dirichlet dverts[2*nd], Neumann nverts[2*nn]) compiled in; `record`: the
 // kernel can record walks (return_history); `n_sources` > 1: the walk scores
 // sources SLOT_F, SLOT_EXTRA.. (multi-source batching).
-// `block`: threads per workgroup the kernel is launched with.
+// `block`: threads per workgroup the kernel is launched with; seg_phi: the
+// device's per-segment normal angles of a compiled-in Neumann polyline (nn - 1
+// floats, read back from the setup kernel so the constants carry its bits).
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record,
-                         int n_sources = 1, int block = 256);
+                         int n_sources = 1, int block = 256, const float* seg_phi = nullptr);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

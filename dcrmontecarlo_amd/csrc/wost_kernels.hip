@@ -79,6 +79,8 @@ struct ProgView {
 
 // Fields read from the program buffer (the precompiled, interpreted path).
 struct InterpFields {
+    static constexpr bool kConstDirichlet = false;   // polylines are staged in LDS
+    static constexpr bool kConstNeumann = false;
     ProgView P;
     DField fG, fF, fS, fA;
     bool det;
@@ -113,6 +115,7 @@ struct InterpFields {
                                                      float r) const {
         return intersect_polylines<false>(sN, nn, x, y, dx, dy, r);
     }
+    __device__ __forceinline__ float neumann_phi(const float* sPhi, int seg) const { return sPhi[seg]; }
 };
 
 #ifndef WOST_WALK_MIN_WAVES
@@ -150,6 +153,7 @@ wost_walk_kernel(const WalkArgs A) {
     }
 
 hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu) {
+    (void)n_points;
     const size_t lds = walk_lds_bytes(mode, nd, nn, n_points);
 #define OCC(n, s, d, t, x) \
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, wost_walk_kernel<n, s, d, t, x>, kWalkBlock, lds)

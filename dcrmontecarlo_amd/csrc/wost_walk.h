@@ -37,7 +37,7 @@ struct WalkArgs {
     float rmin;                  // eps / 2 (solvers/WoStSolver.py:167)
     uint32_t key0, key1;         // Philox key = seed
     int32_t chunk;               // walks claimed per work-queue dequeue
-    int32_t n_points;            // query points (staged in LDS when <= kLdsPointsMax)
+    int32_t n_points;            // query points
     double inv_walks_per_point;  // 1/W for the point index of a walk id
     const float* seg_phi;        // [nn-1] atan2 of each Neumann segment's left normal
     float* rec;                  // walk recorder (return_history), or null: kRecFloats floats per
@@ -62,21 +62,27 @@ constexpr int kWalkBlock = 256;
 // 1 when the step sampled the source.
 constexpr int kRecFloats = WOST_REC_FLOATS;   // include/wost.h, wost_solve_history
 enum RecField { REC_X = 0, REC_Y, REC_DD, REC_DN, REC_SX, REC_SY, REC_C, REC_AUX };
-constexpr int kLdsPointsMax = 1024;
 
 WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
-// Bytes of dynamic LDS a walk-kernel workgroup needs. With the segment tree
-// the Neumann polyline stays in global memory (read through the caches).
-// With the segment tree, its first tree_lds records (64 B each) can be staged
-// too (they follow the query points).
+// Bytes of dynamic LDS a walk-kernel workgroup needs, in layout order:
+//  * G_norm cells (delta tracking; else a 16-byte pad): sample_rho_tail reads the
+//    word before the sampler's tail;
+//  * the sampler's nodes 1..N-1 (node 0 is a kernel argument);
+//  * the Dirichlet vertices, unless the Fields policy has them compiled in;
+//  * the Neumann vertices and segment angles (scan kernels), unless compiled in;
+//  * with the segment tree, its first tree_lds records (64 B each).
+// Query points are read from global memory (once per walk, at refill).
 WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false,
-                                  bool delta = false, int tree_lds = 0) {
-    size_t b = align16(sizeof(float2) * (size_t)nd);
-    if (neu && !tree) b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
-    if (src) b += sizeof(float) * (size_t)kSamplerFloatsPadded;
-    if (delta) b += sizeof(float4) * (size_t)kGnormCells;
-    if (n_points <= kLdsPointsMax) b += align16(sizeof(float2) * (size_t)n_points);
+                                  bool delta = false, int tree_lds = 0, bool const_d = false, bool const_n = false) {
+    (void)n_points;
+    size_t b = 0;
+    if (src) b += delta ? sizeof(float4) * (size_t)kGnormCells : 16;
+    if (src) b += sizeof(float) * (size_t)kSamplerTailFloats;
+    b = align16(b);
+    if (!const_d) b += align16(sizeof(float2) * (size_t)nd);
+    if (neu && !tree && !const_n)
+        b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
     if (tree) b += 4 * sizeof(float4) * (size_t)tree_lds;
     return b;
 }
@@ -85,8 +91,9 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // alpha(x,y), alpha_jet(x,y), detached(), sigma_bar(), sqrt_sigma_bar(),
 // inv_sigma_bar(), and the polyline scans dirichlet_distance(sD,
 // nd, x, y), neumann_silhouette_distance(sN, nn, x, y), neumann_intersect(sN,
-// nn, x, y, dx, dy, r) (the interpreted kernels scan the staged vertices; the
-// specialised ones may have them compiled in). TREE: Neumann queries through
+// nn, x, y, dx, dy, r), neumann_phi(sPhi, seg) (the interpreted kernels scan the
+// staged vertices; the specialised ones may have them compiled in:
+// F::kConstDirichlet / F::kConstNeumann, and then nothing is staged for them). TREE: Neumann queries through
 // the segment tree. REC: the kernel can record walks (A.rec).
 // NS > 1 (multi-source batching): the walk scores NS source
 // fields at once -- the walk itself does not depend on the source, so every
@@ -111,20 +118,23 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #pragma clang fp contract(off)
     static_assert(NS >= 1 && (NS == 1 || SRC) && (NS == 1 || !REC), "multi-source walks need a source, no recorder");
     static_assert(!(FIX && (DELTA || TREE)), "compat=fixed covers the Laplace, Poisson and mixed scan estimators");
-    float2* sD = reinterpret_cast<float2*>(smem);
-    float2* sN = reinterpret_cast<float2*>(smem + align16(sizeof(float2) * (size_t)A.nd));
-    float* sPhi = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sN) +
-                                           ((NEU && !TREE) ? align16(sizeof(float2) * (size_t)A.nn) : 0));
-    float* sT = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(sPhi) +
-                                         ((NEU && !TREE) ? align16(sizeof(float) * (size_t)(A.nn > 1 ? A.nn - 1 : 0)) : 0));
-    float4* sG = reinterpret_cast<float4*>(sT + (SRC ? kSamplerFloatsPadded : 0));   // G_norm cells
-    float2* sP = reinterpret_cast<float2*>(sG + (DELTA ? kGnormCells : 0));
-    const bool points_in_lds = A.n_points <= kLdsPointsMax;
-    float4* sTree = reinterpret_cast<float4*>(reinterpret_cast<unsigned char*>(sP) +
-                                              (points_in_lds ? align16(sizeof(float2) * (size_t)A.n_points) : 0));
+    constexpr bool kStageD = !F::kConstDirichlet;
+    constexpr bool kStageN = NEU && !TREE && (!F::kConstNeumann || FIX);   // FIX scans sN itself
+    unsigned char* lds = smem;
+    float4* sG = reinterpret_cast<float4*>(lds);                          // G_norm cells
+    float* sT = reinterpret_cast<float*>(lds + (DELTA ? sizeof(float4) * (size_t)kGnormCells : 16));  // sampler tail
+    lds += SRC ? align16((DELTA ? sizeof(float4) * (size_t)kGnormCells : 16) + sizeof(float) * kSamplerTailFloats) : 0;
+    float2* sD = reinterpret_cast<float2*>(lds);
+    lds += kStageD ? align16(sizeof(float2) * (size_t)A.nd) : 0;
+    float2* sN = reinterpret_cast<float2*>(lds);
+    lds += kStageN ? align16(sizeof(float2) * (size_t)A.nn) : 0;
+    float* sPhi = reinterpret_cast<float*>(lds);
+    lds += kStageN ? align16(sizeof(float) * (size_t)(A.nn > 1 ? A.nn - 1 : 0)) : 0;
+    float4* sTree = reinterpret_cast<float4*>(lds);
 
-    for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
-    if (NEU && !TREE) {
+    if (kStageD)
+        for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
+    if (kStageN) {
         for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
         for (int i = threadIdx.x; i < A.nn - 1; i += blockDim.x) sPhi[i] = A.seg_phi[i];
     }
@@ -132,14 +142,15 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         for (int i = threadIdx.x; i < 4 * A.tree_lds_records; i += blockDim.x) sTree[i] = A.tree[i];
     const SegTree tree{A.tree, TREE ? sTree : nullptr, TREE ? A.tree_lds_records : 0, A.nverts, A.nn,
                        A.tree_first_leaf, A.tree_leaf, A.tree_tol};
-    if (SRC)
-        for (int i = threadIdx.x; i < WOST_SAMPLER_TABLE_N; i += blockDim.x) sT[i] = A.table[i];
+    float node0 = 0.0f;
+    if (SRC) {
+        node0 = A.table[0];
+        for (int i = threadIdx.x; i < kSamplerTailFloats; i += blockDim.x) sT[i] = A.table[i + 1];
+    }
     if (DELTA) {
         const float4* g = reinterpret_cast<const float4*>(A.table + kSamplerFloatsPadded);
         for (int i = threadIdx.x; i < kGnormCells; i += blockDim.x) sG[i] = g[i];
     }
-    if (points_in_lds)
-        for (int i = threadIdx.x; i < A.n_points; i += blockDim.x) sP[i] = A.points[i];
     __syncthreads();
 
     const float sigma_bar = fld.sigma_bar();
@@ -213,9 +224,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 const int64_t rem = (int64_t)(wid - pid * (uint64_t)A.walks_per_point);
                 if (rem < 0) --pid;
                 else if (rem >= A.walks_per_point) ++pid;
-                float2 q;
-                if (points_in_lds) q = sP[pid];
-                else q = A.points[pid];
+                const float2 q = A.points[pid];
                 px = q.x; py = q.y;
                 k = 0; dD = FIX ? WOST_INF : 1.0f; onB = false; phi = 0.f; w = 1.f;
 #pragma unroll
@@ -263,7 +272,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                               : TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
                                      : fld.neumann_intersect(sN, A.nn, px, py, cs, sn, r);
             xnx = h.x; xny = h.y; onB = h.hit;
-            if (h.hit) phi = TREE ? A.seg_phi[h.seg] : sPhi[h.seg];
+            if (h.hit) phi = TREE ? A.seg_phi[h.seg] : fld.neumann_phi(sPhi, h.seg);
             if (FIX && h.hit) {
                 // inward normal: the left normal when the ray crossed the segment from
                 // its left side, i.e. cross(d, u) > 0 (then dot(left normal, d) < 0)
@@ -281,7 +290,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float gnorm = 0.f;
         Jet aj{0.f, 0.f, 0.f, 0.f};
         if (SRC) {                                                   // :242-258
-            const float rs = sample_rho(sT, u01(rn.y)) * r;          // :244 (sampler, quirks Q3-Q5)
+            const float rs = sample_rho_tail(sT, node0, u01(rn.y)) * r;   // :244 (sampler, quirks Q3-Q5)
             if constexpr (FIX) {                                     // Q13 fixed: own direction
                 const float ts = (u01(rn.w) * 2.0f) * kPiF;
                 const float cs2 = f_cos(ts), sn2 = f_sin(ts);
@@ -297,7 +306,12 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 // needs a2 > b2 (rare: only Neumann hits make the next point closer);
                 // only then evaluate the reference's exact comparison.
                 const float a2 = e1x * e1x + e1y * e1y, b2 = e2x * e2x + e2y * e2y;
-                if (a2 > b2) clipped = sqrtf(a2) > sqrtf(b2);
+                // a real branch (the compiler otherwise evaluates both correctly rounded
+                // square roots for every lane and selects, ~35 instructions per step)
+                if (WOST_ANY(a2 > b2)) {
+                    WOST_NO_SPECULATION();
+                    if (a2 > b2) clipped = sqrtf(a2) > sqrtf(b2);
+                }
                 if (clipped) { yx = xnx; yy = xny; }
             }
             if (DELTA) {
