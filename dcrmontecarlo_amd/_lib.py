@@ -20,8 +20,11 @@ WOST_ERR_HIP = -2
 WOST_ERR_NO_DEVICE = -3
 WOST_ERR_UNSUPPORTED = -4
 WOST_ERR_OOM = -5
+WOST_ERR_COMM = -6
 
-ABI_VERSION = 2   # include/wost.h WOST_ABI_VERSION
+ABI_VERSION = 3   # include/wost.h WOST_ABI_VERSION
+WOST_COMM_ID_BYTES = 128
+WOST_COMM_SUM, WOST_COMM_MAX = 0, 1
 WOST_BLOCK_WALKS = 4096
 WOST_MAX_SOURCES = 16   # include/wost.h
 WOST_SAMPLER_TABLE_N = 4097
@@ -62,6 +65,10 @@ class WostTiming(ctypes.Structure):
                 ("total_walks", c_uint64), ("jit", c_int32), ("tree", c_int32)]
 
 
+class WostDistTiming(ctypes.Structure):
+    _fields_ = [("local", WostTiming), ("walk_begin", c_int64), ("walk_end", c_int64), ("total_steps", c_uint64)]
+
+
 class WostError(RuntimeError):
     """A libwost call failed (HIP error, no device, out of memory)."""
 
@@ -92,6 +99,21 @@ def _load():
                                        c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_float),
                                        POINTER(c_uint32)]),
         "wost_last_timing": (c_int32, [H, POINTER(WostTiming)]),
+        "wost_num_sources": (c_int32, [H, POINTER(c_int32)]),
+        "wost_solve_range": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
+                                       c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_float),
+                                       POINTER(c_uint32)]),
+        "wost_comm_unique_id": (c_int32, [POINTER(c_uint8)]),
+        "wost_comm_create": (c_int32, [POINTER(c_uint8), c_int32, c_int32, c_int32, POINTER(c_void_p)]),
+        "wost_comm_destroy": (None, [c_void_p]),
+        "wost_comm_info": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int32), POINTER(c_int32)]),
+        "wost_comm_last_error": (c_char_p, []),
+        "wost_comm_allgather": (c_int32, [c_void_p, POINTER(c_double), c_int64, POINTER(c_double)]),
+        "wost_comm_allreduce": (c_int32, [c_void_p, POINTER(c_double), c_int64, c_int32]),
+        "wost_comm_barrier": (c_int32, [c_void_p]),
+        "wost_shard_walk_range": (c_int32, [c_int64, c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
+        "wost_solve_distributed": (c_int32, [H, c_void_p, POINTER(c_float), c_int64, c_int64, c_int32, c_float,
+                                             c_uint64, POINTER(c_double), POINTER(WostDistTiming)]),
         "wost_greens_norm": (c_int32, [c_double, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
@@ -118,10 +140,10 @@ def _load():
 lib = _load()
 
 
-def check(rc: int, what: str = "libwost"):
+def check(rc: int, what: str = "libwost", comm: bool = False):
     if rc == WOST_OK:
         return
-    msg = (lib.wost_last_error() or b"").decode(errors="replace")
+    msg = ((lib.wost_comm_last_error() if comm else lib.wost_last_error()) or b"").decode(errors="replace")
     if rc == WOST_ERR_INVALID_ARG:
         raise ValueError(f"{what}: {msg}")
     if rc == WOST_ERR_UNSUPPORTED:

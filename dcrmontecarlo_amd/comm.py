@@ -1,0 +1,133 @@
+"""Multi-GPU solves through libwost's own RCCL communicator (include/wost.h, "Multi-GPU").
+
+One process per GPU. Rank r solves the walk range ``shard_walk_range(W, R, r)`` of
+EVERY point (whole blocks of WOST_BLOCK_WALKS walks, about W / R walks of each point,
+so ranks stay balanced whatever the points' walk lengths), the per-block partial sums
+are all-gathered over RCCL (xGMI on MI355X), and every rank sums them per point in
+global block order: the result is bitwise that of a one-GPU solve for any R
+(SURVEY.md 8e). The reference has no parallel code.
+
+The only thing libwost needs from outside is the 128-byte RCCL unique id, made on one
+rank and handed to the others: ``Communicator.from_torch`` uses an initialised
+torch.distributed group (gloo is enough -- it carries only these bytes),
+``Communicator.from_file`` a file that every rank can read.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import time
+
+import numpy as np
+
+from . import _lib
+
+
+def shard_walk_range(walks_per_point: int, n_ranks: int, rank: int) -> tuple[int, int]:
+    """Rank `rank`'s walk range [begin, end) of each point (wost_shard_walk_range)."""
+    nb = (int(walks_per_point) + _lib.WOST_BLOCK_WALKS - 1) // _lib.WOST_BLOCK_WALKS
+    b0, b1 = nb * rank // n_ranks, nb * (rank + 1) // n_ranks
+    return min(b0 * _lib.WOST_BLOCK_WALKS, walks_per_point), min(b1 * _lib.WOST_BLOCK_WALKS, walks_per_point)
+
+
+def unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * _lib.WOST_COMM_ID_BYTES)()
+    _lib.check(_lib.lib.wost_comm_unique_id(buf), "wost_comm_unique_id", comm=True)
+    return bytes(buf)
+
+
+class Communicator:
+    """An RCCL communicator of libwost (wost_comm_create)."""
+
+    def __init__(self, uid: bytes, n_ranks: int, rank: int, device: int):
+        if len(uid) != _lib.WOST_COMM_ID_BYTES:
+            raise ValueError(f"unique id must be {_lib.WOST_COMM_ID_BYTES} bytes")
+        buf = (ctypes.c_uint8 * _lib.WOST_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.wost_comm_create(buf, int(n_ranks), int(rank), int(device), ctypes.byref(h)),
+                   "wost_comm_create", comm=True)
+        self._c = h
+        self.n_ranks, self.rank, self.device = int(n_ranks), int(rank), int(device)
+
+    @classmethod
+    def from_torch(cls, group=None, device: int | None = None) -> "Communicator":
+        """Bootstrap over an initialised torch.distributed group (only the id travels)."""
+        import torch.distributed as dist
+
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        box = [unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        return cls(box[0], world, rank, device)
+
+    @classmethod
+    def from_file(cls, path: str, n_ranks: int, rank: int, device: int, timeout: float = 120.0) -> "Communicator":
+        """Bootstrap through a file: rank 0 writes the id (atomically), the others wait for it.
+        The caller removes a stale file before rank 0 starts."""
+        if rank == 0:
+            tmp = f"{path}.tmp.{os.getpid()}"
+            with open(tmp, "wb") as f:
+                f.write(unique_id())
+            os.replace(tmp, path)
+        t0 = time.time()
+        while True:
+            try:
+                with open(path, "rb") as f:
+                    uid = f.read()
+                if len(uid) == _lib.WOST_COMM_ID_BYTES:
+                    break
+            except OSError:
+                pass
+            if time.time() - t0 > timeout:
+                raise TimeoutError(f"no communicator id in {path} after {timeout} s")
+            time.sleep(0.05)
+        return cls(uid, n_ranks, rank, device)
+
+    def close(self):
+        if getattr(self, "_c", None) is not None and self._c.value:
+            _lib.lib.wost_comm_destroy(self._c)
+            self._c = None
+
+    __del__ = close
+
+    def allgather(self, a: np.ndarray) -> np.ndarray:
+        """[n_ranks, *a.shape] float64: every rank's array, in rank order."""
+        a = np.ascontiguousarray(a, np.float64)
+        out = np.empty((self.n_ranks,) + a.shape, np.float64)
+        _lib.check(_lib.lib.wost_comm_allgather(self._c, _lib.dptr(a), a.size, _lib.dptr(out)),
+                   "wost_comm_allgather", comm=True)
+        return out
+
+    def allreduce(self, a, op: str = "sum") -> np.ndarray:
+        a = np.array(a, np.float64, copy=True, ndmin=1)
+        _lib.check(_lib.lib.wost_comm_allreduce(self._c, _lib.dptr(a), a.size,
+                                                _lib.WOST_COMM_SUM if op == "sum" else _lib.WOST_COMM_MAX),
+                   "wost_comm_allreduce", comm=True)
+        return a
+
+    def barrier(self):
+        _lib.check(_lib.lib.wost_comm_barrier(self._c), "wost_comm_barrier", comm=True)
+
+
+def solve_distributed(solver, comm: Communicator, points, nWalks: int, maxSteps: int = 1000, eps: float = 1e-4,
+                      seed: int = 0):
+    """WostSolver_2D.solve across the communicator's ranks (collective; every rank passes
+    the same arguments). Returns (u [N,1] float32, SolveStats, timing dict) on every rank;
+    u and the statistics are bitwise those of a one-GPU solve."""
+    from .solvers.WoStSolver import stats_from_sums
+
+    p = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 2))
+    n = p.shape[0]
+    ns = ctypes.c_int32(1)
+    _lib.check(_lib.lib.wost_num_sources(solver._h, ctypes.byref(ns)), "wost_num_sources")
+    sums = np.zeros((n, 2 * ns.value + 1), np.float64)
+    t = _lib.WostDistTiming()
+    _lib.check(_lib.lib.wost_solve_distributed(solver._h, comm._c, _lib.fptr(p), n, int(nWalks), int(maxSteps),
+                                               float(eps), int(seed) & (2**64 - 1), _lib.dptr(sums), ctypes.byref(t)),
+               "wost_solve_distributed", comm=True)
+    timing = {k: getattr(t.local, k) for k, _ in _lib.WostTiming._fields_}
+    timing.update({"walk_begin": int(t.walk_begin), "walk_end": int(t.walk_end), "all_steps": int(t.total_steps)})
+    solver.last_timing = timing
+    st = stats_from_sums(sums[:, [0, 1, -1]] if sums.shape[1] > 3 else sums, int(nWalks))
+    return st.mean.astype(np.float32).reshape(n, 1), st, timing

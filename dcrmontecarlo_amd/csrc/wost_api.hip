@@ -647,6 +647,12 @@ int wost_greens_norm(double sigma_bar, const float* radii, int64_t n, float* out
     return WOST_OK;
 }
 
+int wost_num_sources(const wost_handle* h, int32_t* n_sources) {
+    if (!h || !n_sources) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    *n_sources = h->n_sources;
+    return WOST_OK;
+}
+
 int wost_last_timing(const wost_handle* h, wost_timing* out) {
     if (!h || !out) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
     *out = h->timing;
@@ -661,9 +667,13 @@ constexpr int64_t kMaxRecordBatchBytes = int64_t(1) << 30;   // device buffer of
 
 // wost_solve, and with `records` != null also the walk recorder
 // (wost_solve_history): records[walk][max_steps + 1][kRecFloats] on the host.
+// Walk-range mode (wost_solve_range): walk_begin/walk_end != 0/W solves walks
+// [walk_begin, walk_end) of every point; blocks are then (point, block of the
+// range), point-major, and block_begin/block_end are ignored.
 int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W, int64_t block_begin,
                int64_t block_end, int32_t max_steps, float eps, uint64_t seed, double* block_stats,
-               double* point_stats, float* walk_values, uint32_t* walk_steps, float* records, bool multi = false) {
+               double* point_stats, float* walk_values, uint32_t* walk_steps, float* records, bool multi = false,
+               int64_t walk_begin = 0, int64_t walk_end = -1) {
     if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
     const int ns = h->n_sources;
     if (ns != 1 && !multi)
@@ -677,7 +687,19 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         return fail(WOST_ERR_INVALID_ARG, "n_points * nWalks must stay below 2^53 walks");
     const int64_t nbpp = (W + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
     const int64_t nb_total = n_points * nbpp;
-    if (block_begin < 0 || block_end < block_begin || block_end > nb_total)
+    if (walk_end < 0) walk_end = W;
+    const bool range = walk_begin != 0 || walk_end != W;
+    if (range && (walk_begin < 0 || walk_end <= walk_begin || walk_end > W || walk_begin % WOST_BLOCK_WALKS != 0 ||
+                  (walk_end % WOST_BLOCK_WALKS != 0 && walk_end != W)))
+        return fail(WOST_ERR_INVALID_ARG,
+                    "walk range [%lld,%lld) of %lld walks must be non-empty with block-aligned ends (multiples of %d, "
+                    "or the end at W)", (long long)walk_begin, (long long)walk_end, (long long)W, WOST_BLOCK_WALKS);
+    const int64_t Wr = walk_end - walk_begin;                            // walks per point solved
+    const int64_t nbr = (Wr + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;   // blocks per point solved
+    if (range) {
+        block_begin = 0;
+        block_end = n_points * nbr;
+    } else if (block_begin < 0 || block_end < block_begin || block_end > nb_total)
         return fail(WOST_ERR_INVALID_ARG, "block range [%lld,%lld) outside [0,%lld)", (long long)block_begin,
                     (long long)block_end, (long long)nb_total);
     for (int64_t i = 0; i < 2 * n_points; ++i)
@@ -707,7 +729,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         return p * W + std::min<int64_t>((b + 1) * WOST_BLOCK_WALKS, W);
     };
 
-    const int64_t walks_total = blk_end(block_end - 1) - blk_begin(block_begin);
+    const int64_t walks_total = range ? n_points * Wr : blk_end(block_end - 1) - blk_begin(block_begin);
     // walks per launch: the recorder's device buffer bounds it
     int64_t batch_limit = kMaxBatchWalks / ns;
     const int64_t rec_stride = (int64_t)max_steps + 1;
@@ -719,6 +741,9 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
                         "return_history: %lld recorded steps per walk need more than %lld bytes per walk block; "
                         "lower maxSteps or nWalks", (long long)rec_stride, (long long)kMaxRecordBatchBytes);
     }
+    if (range && Wr > batch_limit)
+        return fail(WOST_ERR_INVALID_ARG, "walk range of %lld walks per point exceeds one launch (%lld walks)",
+                    (long long)Wr, (long long)batch_limit);
     if ((rc = ensure_cap(h->d_points, h->points_cap, std::max<int64_t>(n_points, 1))) != WOST_OK) return rc;
     HIP_TRY(hipMemcpyAsync(h->d_points, points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
     if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, batch_limit), ns)) != WOST_OK) return rc;
@@ -790,16 +815,33 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     int launches = 0;
     double walk_ms = 0.0, red_ms = 0.0;
     while (j < block_end) {
-        // gather whole blocks into a batch of at most kMaxBatchWalks walks
-        const int64_t wb = blk_begin(j);
-        int64_t j2 = j;
+        int64_t j2 = j, count = 0;
         begins.clear();
-        while (j2 < block_end && blk_end(j2) - wb <= batch_limit) {
-            begins.push_back(blk_begin(j2) - wb);
-            ++j2;
+        if (range) {
+            // whole points' ranges: local walk l is walk walk_begin + l % Wr of point p0 + l / Wr
+            const int64_t p0 = j / nbr;
+            const int64_t p1 = std::min<int64_t>(n_points, p0 + std::max<int64_t>(1, batch_limit / Wr));
+            for (int64_t p = p0; p < p1; ++p)
+                for (int64_t b = 0; b < nbr; ++b) begins.push_back((p - p0) * Wr + b * WOST_BLOCK_WALKS);
+            count = (p1 - p0) * Wr;
+            j2 = p1 * nbr;
+            a.wid_begin = 0;
+            a.range_walks = Wr;
+            a.range_offset = walk_begin;
+            a.range_point0 = p0;
+            a.inv_range_walks = 1.0 / (double)Wr;
+        } else {
+            // gather whole blocks into a batch of at most kMaxBatchWalks walks
+            const int64_t wb = blk_begin(j);
+            while (j2 < block_end && blk_end(j2) - wb <= batch_limit) {
+                begins.push_back(blk_begin(j2) - wb);
+                ++j2;
+            }
+            if (j2 == j) return fail(WOST_ERR_INVALID_ARG, "internal: block larger than a batch");
+            count = blk_end(j2 - 1) - wb;
+            a.wid_begin = wb;
+            a.range_walks = 0;
         }
-        if (j2 == j) return fail(WOST_ERR_INVALID_ARG, "internal: block larger than a batch");
-        const int64_t count = blk_end(j2 - 1) - wb;
         begins.push_back(count);
         const int64_t nb = j2 - j;
 
@@ -809,7 +851,6 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
 
         a.out_val = h->d_val;
         a.out_steps = h->d_steps;
-        a.wid_begin = wb;
         a.count = count;
         const int64_t max_grid = (int64_t)blocks_per_cu * h->num_cus;
         const int64_t want = (count + block - 1) / block;
@@ -858,7 +899,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     for (int64_t b = 0; b < nblk; ++b) {
         steps_sum += (uint64_t)bs[row * b + row - 1];
         if (point_stats) {
-            const int64_t p = (block_begin + b) / nbpp;
+            const int64_t p = (block_begin + b) / (range ? nbr : nbpp);
             for (int c = 0; c < row; ++c) point_stats[row * p + c] += bs[row * b + c];
         }
     }
@@ -883,6 +924,18 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
                double* block_stats, double* point_stats, float* walk_values, uint32_t* walk_steps) {
     return solve_impl(h, points, n_points, W, block_begin, block_end, max_steps, eps, seed, block_stats,
                       point_stats, walk_values, walk_steps, nullptr);
+}
+
+int wost_solve_range(wost_handle* h, const float* points, int64_t n_points, int64_t W, int64_t walk_begin,
+                     int64_t walk_end, int32_t max_steps, float eps, uint64_t seed, double* block_stats,
+                     double* point_stats, float* walk_values, uint32_t* walk_steps) {
+    if (walk_begin == 0 && walk_end == W) {   // the whole range: an ordinary solve
+        const int64_t nb = wost_num_blocks(n_points, W);
+        return solve_impl(h, points, n_points, W, 0, nb, max_steps, eps, seed, block_stats, point_stats,
+                          walk_values, walk_steps, nullptr, true);
+    }
+    return solve_impl(h, points, n_points, W, 0, 0, max_steps, eps, seed, block_stats, point_stats, walk_values,
+                      walk_steps, nullptr, true, walk_begin, walk_end);
 }
 
 int wost_solve_history(wost_handle* h, const float* points, int64_t n_points, int64_t W, int32_t max_steps,

@@ -50,6 +50,13 @@ struct WalkArgs {
     float tree_stop2;            // largest float whose sqrtf is <= rmin (< 0: none); silhouette_distance_tree
     int32_t tree_lds_records;    // the first records of the tree staged in LDS (0: none)
     int32_t pad_;
+    // walk-range batches (wost_solve_range): when range_walks > 0, local walk l is walk
+    // range_offset + l % range_walks of point range_point0 + l / range_walks, i.e. global
+    // id (range_point0 + l / range_walks) * walks_per_point + range_offset + l % range_walks
+    int64_t range_walks;
+    int64_t range_offset;
+    int64_t range_point0;
+    double inv_range_walks;
 };
 
 constexpr int kWalkBlock = 256;
@@ -167,7 +174,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 
     // per-lane walk state (solvers/WoStSolver.py:188-195)
     bool active = false;
-    uint64_t wid = 0;
+    uint64_t wid = 0;           // global walk id: the Philox subsequence
+    uint64_t lid = 0;           // local walk index: the output slot
     float px = 0.f, py = 0.f;
     float dD = 1.0f;            // dDirichlet seeded with 1.0 (:190, quirk Q12)
     int k = 0;                  // step_count
@@ -186,7 +194,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             if (DELTA) g = g * w;
 #pragma unroll
             for (int s = 0; s < NS; ++s) total[s] = total[s] + g;
-            const int64_t li = (int64_t)(wid - (uint64_t)A.wid_begin);
+            const int64_t li = (int64_t)lid;
             if (REC && A.rec != nullptr) {
                 float* rr = A.rec + ((size_t)li * (size_t)A.rec_stride + (size_t)k) * kRecFloats;
                 rr[REC_X] = px; rr[REC_Y] = py; rr[REC_C] = g; rr[REC_AUX] = total[0];   // end record
@@ -217,13 +225,24 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             const uint32_t take = avail < (uint64_t)n ? (uint32_t)avail : n;
             const uint32_t rank = (uint32_t)__popcll(need & lanes_below);
             if ((need & lanebit) && rank < take) {
-                wid = (uint64_t)A.wid_begin + c_next + rank;
-                // pid = wid / W without a 64-bit integer division: a double
-                // estimate (exact operands below 2^53) and one correction
-                uint64_t pid = (uint64_t)((double)wid * A.inv_walks_per_point);
-                const int64_t rem = (int64_t)(wid - pid * (uint64_t)A.walks_per_point);
-                if (rem < 0) --pid;
-                else if (rem >= A.walks_per_point) ++pid;
+                lid = c_next + rank;
+                // integer quotients without a 64-bit division: a double estimate
+                // (exact operands below 2^53) and one correction
+                uint64_t pid;
+                if (A.range_walks > 0) {
+                    uint64_t q = (uint64_t)((double)lid * A.inv_range_walks);
+                    int64_t rem = (int64_t)(lid - q * (uint64_t)A.range_walks);
+                    if (rem < 0) { --q; rem += A.range_walks; }
+                    else if (rem >= A.range_walks) { ++q; rem -= A.range_walks; }
+                    pid = (uint64_t)A.range_point0 + q;
+                    wid = pid * (uint64_t)A.walks_per_point + (uint64_t)A.range_offset + (uint64_t)rem;
+                } else {
+                    wid = (uint64_t)A.wid_begin + lid;
+                    pid = (uint64_t)((double)wid * A.inv_walks_per_point);
+                    const int64_t rem = (int64_t)(wid - pid * (uint64_t)A.walks_per_point);
+                    if (rem < 0) --pid;
+                    else if (rem >= A.walks_per_point) ++pid;
+                }
                 const float2 q = A.points[pid];
                 px = q.x; py = q.y;
                 k = 0; dD = FIX ? WOST_INF : 1.0f; onB = false; phi = 0.f; w = 1.f;
@@ -347,7 +366,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         if (REC && A.rec != nullptr) {                               // :218-222, :261-266
             // the tree's silhouette distance is exact only below dD: recompute it
             if (TREE) dnv = silhouette_distance_tree(tree, px, py, WOST_INF);
-            const int64_t li = (int64_t)(wid - (uint64_t)A.wid_begin);
+            const int64_t li = (int64_t)lid;
             float4* rr = reinterpret_cast<float4*>(A.rec + ((size_t)li * (size_t)A.rec_stride + (size_t)k) * kRecFloats);
             rr[0] = float4{px, py, dd, dnv};
             rr[1] = float4{yx, yy, cv, SRC ? 1.0f : 0.0f};

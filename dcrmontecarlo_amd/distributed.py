@@ -1,18 +1,62 @@
-"""Multi-GPU solve: one process per GPU, walk blocks sharded, one RCCL collective.
+"""Sharding arithmetic of multi-GPU solves, and a torch.distributed variant.
 
-The walks of a solve are grouped in blocks of WOST_BLOCK_WALKS consecutive
-walks of one point (global walk id = point * nWalks + walk). Rank r of R
-solves the contiguous block range [r*NB/R, (r+1)*NB/R) on its own GPU; the
-per-block (sum, sum of squares, steps) rows are exchanged with one
-``all_gather`` (backend "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU for
-tests) and every rank sums them per point in block order. Random streams are
-keyed by global walk id, so the result is bitwise identical for any R.
+The product path is dcrmontecarlo_amd.comm: libwost's own RCCL communicator and
+wost_solve_distributed (rank r solves the walk range shard_walk_range(W, R, r) of
+every point, one all-gather of the block sums, per-point sums in global block
+order -- bitwise the one-GPU result). This module holds the host-side mirror of
+that merge (merge_walk_range_blocks, block_stats_of_walks: the gloo CPU tests
+drive real shards of oracle walks through it), the weak-scaling replication
+helpers of bench.py, and an optional torch.distributed path (contiguous block
+ranges, all_gather of the rows through torch's backend) for callers that
+already run a torch process group.
 """
 from __future__ import annotations
 
 import numpy as np
 
 from .solvers.WoStSolver import stats_from_sums
+
+
+def shard_walk_range(walks_per_point: int, world: int, rank: int) -> tuple[int, int]:
+    """Rank `rank`'s walk range of every point: whole blocks, evenly split
+    (wost_shard_walk_range; dcrmontecarlo_amd.comm.shard_walk_range)."""
+    B = 4096   # WOST_BLOCK_WALKS
+    nb = (int(walks_per_point) + B - 1) // B
+    b0, b1 = nb * rank // world, nb * (rank + 1) // world
+    return min(b0 * B, walks_per_point), min(b1 * B, walks_per_point)
+
+
+def block_stats_of_walks(values: np.ndarray, steps: np.ndarray, walk_begin: int) -> np.ndarray:
+    """(sum, sum^2, steps) of each WOST_BLOCK_WALKS block of per-walk values [N, Wr]
+    whose first walk is walk_begin (block-aligned): [N, blocks, 3], summed in walk
+    order (a host stand-in for the device reduction)."""
+    B = 4096
+    v = np.asarray(values, np.float64)
+    s = np.asarray(steps, np.float64)
+    n, wr = v.shape
+    nb = (wr + B - 1) // B
+    out = np.zeros((n, nb, 3))
+    for b in range(nb):
+        sl = slice(b * B, min((b + 1) * B, wr))
+        out[:, b, 0] = v[:, sl].sum(1)
+        out[:, b, 1] = (v[:, sl] ** 2).sum(1)
+        out[:, b, 2] = s[:, sl].sum(1)
+    return out
+
+
+def merge_walk_range_blocks(parts, walks_per_point: int) -> np.ndarray:
+    """Per-point sums from every rank's [N, blocks_r, 3] block rows (rank order): rank
+    0's blocks, then rank 1's, ... -- the global block order of one GPU -- added to
+    0.0 one block at a time, exactly as wost_solve_distributed does."""
+    world = len(parts)
+    n = parts[0].shape[0]
+    acc = np.zeros((n, parts[0].shape[2]))
+    for r in range(world):
+        w0, w1 = shard_walk_range(walks_per_point, world, r)
+        nb = (w1 - w0 + 4095) // 4096 if w1 > w0 else 0
+        for b in range(nb):
+            acc += parts[r][:, b]
+    return acc
 
 
 def shard_range(n_blocks: int, rank: int, world: int) -> tuple[int, int]:

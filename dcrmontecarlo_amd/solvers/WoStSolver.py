@@ -253,6 +253,21 @@ class WostSolver_2D:
         self.last_timing = self.timing()
         return bs
 
+    def solve_range(self, solvePoints, nWalks: int, walk_begin: int, walk_end: int, maxSteps: int = 1000,
+                    eps: float = 1e-4, seed: int = 0):
+        """Walks [walk_begin, walk_end) of every point (block-aligned ends; wost_solve_range):
+        the (sum, sum^2, steps) rows of its blocks, [N, blocks, 3], each equal to the
+        corresponding block of the full solve. The unit of dcrmontecarlo_amd.comm's sharding."""
+        p = _points_np(solvePoints)
+        n = p.shape[0]
+        nbr = -(-(int(walk_end) - int(walk_begin)) // _lib.WOST_BLOCK_WALKS)
+        bs = np.zeros((n, max(nbr, 0), 3), np.float64)
+        _lib.check(_lib.lib.wost_solve_range(self._h, _lib.fptr(p), n, int(nWalks), int(walk_begin), int(walk_end),
+                                             int(maxSteps), float(eps), int(seed) & (2**64 - 1), _lib.dptr(bs), None,
+                                             None, None), "WostSolver_2D.solve_range")
+        self.last_timing = self.timing()
+        return bs
+
     def set_jit(self, enable: bool):
         """Use the field-specialised (hiprtc) walk kernel (default) or the precompiled
         kernel that interprets the fields. Both give identical results."""

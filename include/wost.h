@@ -30,7 +30,7 @@ typedef unsigned long long uint64_t;
 extern "C" {
 #endif
 
-#define WOST_ABI_VERSION 2
+#define WOST_ABI_VERSION 3
 
 /* Most source fields one multi-source solve can score (wost_set_sources). */
 #define WOST_MAX_SOURCES 16
@@ -54,12 +54,13 @@ enum wost_status {
     WOST_ERR_HIP = -2,
     WOST_ERR_NO_DEVICE = -3,
     WOST_ERR_UNSUPPORTED = -4,
-    WOST_ERR_OOM = -5
+    WOST_ERR_OOM = -5,
+    WOST_ERR_COMM = -6          /* RCCL failure (multi-GPU) */
 };
 
 /* compat: "reference" reproduces the reference's estimator including its
- * quirks. "fixed" is reserved for the corrected
- * estimator and is rejected with WOST_ERR_UNSUPPORTED in this ABI version. */
+ * quirks. "fixed" runs the corrected estimator
+ * (Q1-Q5, Q7, Q12, Q13 corrected). */
 enum wost_compat { WOST_COMPAT_REFERENCE = 0, WOST_COMPAT_FIXED = 1 };
 
 /* ---------------------------------------------------------------------------
@@ -249,6 +250,69 @@ int wost_solve_multi(wost_handle* h, const float* points, int64_t n_points,
                      float* walk_values, uint32_t* walk_steps);
 
 int wost_last_timing(const wost_handle* h, wost_timing* out);
+
+/* Number of source fields the handle scores (1, or n of wost_set_sources). */
+int wost_num_sources(const wost_handle* h, int32_t* n_sources);
+
+/* Walks [walk_begin, walk_end) of every point (of walks_per_point per point; the
+ * ends are multiples of WOST_BLOCK_WALKS, or walk_end == walks_per_point): a shard
+ * of a solve that covers every point. Global walk ids, random streams and blocks
+ * are those of the full solve: block b of point p here is the full solve's block
+ * walk_begin / WOST_BLOCK_WALKS + b of that point, with the same sums.
+ *   block_stats [n_points][n_range_blocks][2S+1] (point-major), point_stats
+ *   [n_points][2S+1], walk_values [n_points][walk_end - walk_begin][S], walk_steps
+ *   [n_points][walk_end - walk_begin]  (S = wost_num_sources).
+ * Per point at most 2^26 / S walks (one launch). */
+int wost_solve_range(wost_handle* h, const float* points, int64_t n_points,
+                     int64_t walks_per_point, int64_t walk_begin, int64_t walk_end,
+                     int32_t max_steps, float eps, uint64_t seed,
+                     double* block_stats, double* point_stats,
+                     float* walk_values, uint32_t* walk_steps);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU: one process per GPU, RCCL over xGMI. The reference
+ * has no parallel code; walks shard trivially, and the only exchange is one
+ * all-gather of the per-block partial sums.
+ *   1. one rank calls wost_comm_unique_id and shares the WOST_COMM_ID_BYTES bytes
+ *      with the others (any channel: a file, a TCP store, MPI);
+ *   2. every rank calls wost_comm_create(id, n_ranks, rank, its device);
+ *   3. every rank calls wost_solve_distributed with the same points: rank r solves
+ *      the walk range wost_shard_walk_range(W, n_ranks, r) of EVERY point (each
+ *      rank gets about W / n_ranks walks of each point: balanced whatever the
+ *      points' walk lengths), the block sums are all-gathered, and every rank sums
+ *      them per point in global block order -- point_stats is bitwise that of a
+ *      one-GPU solve, for any number of ranks.
+ * ------------------------------------------------------------------------- */
+#define WOST_COMM_ID_BYTES 128
+typedef struct wost_comm wost_comm;
+enum wost_comm_op { WOST_COMM_SUM = 0, WOST_COMM_MAX = 1 };
+
+typedef struct {
+    wost_timing local;          /* this rank's solve (walk kernel time, steps) */
+    int64_t walk_begin, walk_end;   /* this rank's walk range of every point */
+    uint64_t total_steps;       /* walk-steps of all ranks */
+} wost_dist_timing;
+
+int wost_comm_unique_id(uint8_t* id);
+int wost_comm_create(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, wost_comm** out);
+void wost_comm_destroy(wost_comm* c);
+int wost_comm_info(const wost_comm* c, int32_t* n_ranks, int32_t* rank, int32_t* device);
+const char* wost_comm_last_error(void);
+/* recv[n_ranks * count] = every rank's send[count], in rank order (host buffers). */
+int wost_comm_allgather(wost_comm* c, const double* send, int64_t count, double* recv);
+/* inout[count] reduced over the ranks (op: WOST_COMM_SUM / WOST_COMM_MAX). */
+int wost_comm_allreduce(wost_comm* c, double* inout, int64_t count, int32_t op);
+int wost_comm_barrier(wost_comm* c);
+/* Rank `rank`'s walk range [*walk_begin, *walk_end) of a point's walks_per_point
+ * walks: whole blocks, split as evenly as possible (no device needed). */
+int wost_shard_walk_range(int64_t walks_per_point, int32_t n_ranks, int32_t rank, int64_t* walk_begin,
+                          int64_t* walk_end);
+/* The solve of every point with walks_per_point walks across the communicator's
+ * ranks (collective: every rank calls it with the same arguments); point_stats
+ * [n_points][2S+1] on every rank; timing may be NULL. */
+int wost_solve_distributed(wost_handle* h, wost_comm* c, const float* points, int64_t n_points,
+                           int64_t walks_per_point, int32_t max_steps, float eps, uint64_t seed,
+                           double* point_stats, wost_dist_timing* timing);
 
 /* Walk kernels: by default libwost compiles a field-specialised walk kernel per
  * handle and kernel variant with hiprtc (cached in memory and in

@@ -77,3 +77,87 @@ def test_shard_ranges_partition_blocks():
             ranges = [D.shard_range(nb, r, world) for r in range(world)]
             assert ranges[0][0] == 0 and ranges[-1][1] == nb
             assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+
+
+# ---------------------------------------------------------------- walk-range shards of real walks
+# the layout of libwost's wost_solve_distributed (dcrmontecarlo_amd.comm): rank r solves
+# walks shard_walk_range(W, R, r) of EVERY point; here the walks are the CPU oracle's
+# (same Philox streams as the device), the rows travel through gloo, and the merge is the
+# host mirror of the library's
+def _oracle_range_blocks(sc, pts, W, w0, w1, seed):
+    from oracle import oracle as O
+
+    pb = O.Problem.from_scenario(sc)
+    vals, steps = [], []
+    for p in range(len(pts)):
+        v, s = pb.solve_walks(pts, W, sc.max_steps, sc.eps, seed, wid_begin=p * W + w0, wid_end=p * W + w1,
+                              threads=1)
+        vals.append(v)
+        steps.append(s)
+    return D.block_stats_of_walks(np.array(vals), np.array(steps), w0)
+
+
+def _range_worker(rank, world, port, W, out_q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from dcrmontecarlo_amd import scenarios as S
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = S.poisson_square()
+    pts = sc.points[:3]
+    w0, w1 = D.shard_walk_range(W, world, rank)
+    mine = _oracle_range_blocks(sc, pts, W, w0, w1, 99)
+    nb_max = -(-(-(-W // 4096)) // world)
+    pad = np.zeros((len(pts), nb_max, 3))
+    pad[:, :mine.shape[1]] = mine
+    outs = [torch.empty(pad.shape, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(outs, torch.from_numpy(pad))
+    parts = [o.numpy() for o in outs]
+    out_q.put((rank, D.merge_walk_range_blocks(parts, W)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_walk_range_shards_of_oracle_walks_merge_to_one_rank(world):
+    """Every rank solves its walk range of every point (oracle walks), the padded block
+    rows are all-gathered, and the merged per-point sums equal one rank's bit for bit;
+    the shards cover every walk exactly once."""
+    from dcrmontecarlo_amd import scenarios as S
+
+    W = 3 * 4096 + 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_range_worker, args=(r, world, port, W, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sc = S.poisson_square()
+    single = D.merge_walk_range_blocks([_oracle_range_blocks(sc, sc.points[:3], W, 0, W, 99)], W)
+    for r in range(world):
+        assert np.array_equal(res[r], single)
+    ranges = [D.shard_walk_range(W, world, r) for r in range(world)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == W and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    assert all(a % 4096 == 0 for a, _ in ranges)
+    assert np.all(single[:, 2] >= W)                  # every walk took at least one step
+
+
+def test_walk_range_shards_match_the_library():
+    """The host mirror of the shard arithmetic equals libwost's (no device needed)."""
+    import ctypes
+
+    from dcrmontecarlo_amd import _lib
+    from dcrmontecarlo_amd import comm
+
+    for W in (1, 4095, 4096, 12288, 1_000_000, 1 << 20):
+        for R in (1, 2, 3, 4, 8):
+            for r in range(R):
+                a, b = ctypes.c_int64(), ctypes.c_int64()
+                assert _lib.lib.wost_shard_walk_range(W, R, r, ctypes.byref(a), ctypes.byref(b)) == 0
+                assert (a.value, b.value) == D.shard_walk_range(W, R, r) == comm.shard_walk_range(W, R, r)

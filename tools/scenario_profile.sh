@@ -10,7 +10,7 @@ O="$R/gpurun_out/prof_$SC"
 mkdir -p "$O"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 CMD="$R/tools/scenario_bench.py --only $SC --reps 1 $*"
-AVAIL="$R/gpurun_out/counters.txt"
+AVAIL="$R/profiles/gfx950_counters.txt"
 have() { [ -s "$AVAIL" ] && grep -q "\b$1\b" "$AVAIL"; }
 specs=(
   "${SC}_stats|240|rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 $CMD"
