@@ -5,15 +5,18 @@ Workload (BASELINE.json configs[3]): the DCR dipole survey of
 tests/testGeophysicalScenario.py -- 48 surface electrodes x 1M walks each,
 delta tracking with the reference's conductivity field, mixed Dirichlet /
 Neumann boundary, eps = 0.9, maxSteps = 500. One bench "step" is one full
-survey solve (48M walks, ~3.65G walk-steps) per GPU. With N ranks (weak
-scaling) the job is the survey with N x 1M walks per electrode: the electrode
-list is replicated N times (distributed.replicate_points), rank r solves copy r
--- the one-GPU workload on its own walk ids -- and the per-block partial sums
-are combined with one RCCL all_gather over xGMI (the only data-path
-collective), summed in block order and merged in rank order. The result is
-bitwise that of one GPU solving the replicated list.
+survey solve (48M walks, ~3.65G walk-steps) per GPU.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+N ranks (one process per GPU) solve through libwost's own RCCL communicator
+(dcrmontecarlo_amd.comm, wost_solve_distributed): rank r solves the walk range
+wost_shard_walk_range(W, N, r) of EVERY electrode, the per-block partial sums
+are all-gathered over xGMI (the only data-path collective) and summed per
+electrode in global block order -- bitwise a one-GPU solve of W walks per
+electrode. --scaling weak (default): W = N x 1M, so each GPU keeps the one-GPU
+workload; --scaling strong: W = 1M split N ways. The communicator's id travels
+through the launcher's TCP store; no torch process group is created.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
        (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 Prints one JSON line on rank 0.
 """
@@ -39,6 +42,8 @@ def parse():
     ap.add_argument("--walks", type=int, default=1_000_000, help="walks per electrode")
     ap.add_argument("--electrodes", type=int, default=48)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: N x --walks walks per electrode on N GPUs (default); strong: --walks on N GPUs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-rho", action="store_true", help="skip the apparent-resistivity leg (profiling runs)")
     return ap.parse_args()
@@ -216,15 +221,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    from dcrmontecarlo_amd import distributed as D
+    from dcrmontecarlo_amd import comm as C
     from dcrmontecarlo_amd import perfmodel
     from dcrmontecarlo_amd import scenarios as S
     from dcrmontecarlo_amd import survey
@@ -232,23 +230,27 @@ def main():
 
     sc = S.dcr_dipole(n_electrodes=args.electrodes, n_walks=args.walks)
     solver = sc.solver(device=local)
-    W = sc.n_walks                               # walks per electrode per GPU
-    pts = D.replicate_points(sc.points, world)   # weak scaling: one survey copy per rank
-    nb = solver.num_blocks(len(pts), W)
-    b0, b1 = D.shard_range(nb, rank, world)
+    # libwost's own RCCL communicator (wost_comm_*): the 128-byte id travels through the
+    # launcher's TCP store; barriers, the block-sum all-gather and the max over ranks
+    # are RCCL collectives on libwost's stream -- no torch process group
+    comm = C.Communicator.from_env(device=local) if world > 1 else None
+    # weak: N x 1M walks per electrode over N GPUs; strong: 1M walks per electrode over N
+    Wt = sc.n_walks * (world if args.scaling == "weak" else 1)   # walks per electrode of the whole job
+    w0, w1 = C.shard_walk_range(Wt, world, rank)
 
     def barrier_sync():
-        if dist is not None:
-            import torch
-
-            dist.barrier()
-            torch.cuda.synchronize()
+        # every solve returns with its results on the host (libwost syncs its stream);
+        # the RCCL barrier syncs the communicator's stream before returning
+        if comm is not None:
+            comm.barrier()
 
     def one_step(seed, slv=solver):
-        bs = slv.solve_blocks(pts, W, b0, b1, sc.max_steps, sc.eps, seed=seed)
-        t = slv.last_timing
-        full = D.gather_block_stats(bs, nb, device=f"cuda:{local}") if dist is not None else bs   # RCCL all_gather
-        return D.merge_replicas(D.point_sums(full, len(pts)), world), t
+        """One survey solve; the per-electrode (sum, sum^2, steps) end up in slv.last_point_sums."""
+        if comm is None:
+            slv.solve(sc.points, nWalks=Wt, maxSteps=sc.max_steps, eps=sc.eps, seed=seed)
+        else:
+            C.solve_distributed(slv, comm, sc.points, Wt, sc.max_steps, sc.eps, seed=seed)
+        return slv.last_timing
 
     for k in range(args.warmup):
         one_step(1000 + k)
@@ -259,9 +261,8 @@ def main():
     kernel_ms = 0.0
     launches = 0
     jit = 0
-    sums = None
     for k in range(args.steps):
-        sums, t = one_step(k)
+        t = one_step(k)
         steps_local += int(t["total_steps"])
         kernel_ms += float(t["walk_kernel_ms"])
         launches += int(t["n_launches"])
@@ -271,16 +272,10 @@ def main():
 
     total_steps = steps_local
     max_elapsed = elapsed
-    if dist is not None:
-        import torch
-
-        v = torch.tensor([float(steps_local), elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        s_all = v.clone()
-        dist.all_reduce(s_all[0:1], op=dist.ReduceOp.SUM)
-        e_max = v[1:2].clone()
-        dist.all_reduce(e_max, op=dist.ReduceOp.MAX)
-        total_steps = int(s_all[0].item())
-        max_elapsed = float(e_max.item())
+    if comm is not None:
+        total_steps = int(comm.allreduce([float(steps_local)], "sum")[0])
+        max_elapsed = float(comm.allreduce([elapsed], "max")[0])
+    last_sums = solver.last_point_sums
 
     # apparent resistivity (second half of the metric), outside the timed region: the
     # homogeneous-background survey on the same walk streams as the last timed step
@@ -288,17 +283,17 @@ def main():
     solver_h = sums_h = None
     if not args.no_rho:
         solver_h = survey.homogeneous_solver(sc, ALPHA_BG, solver, device=local)
-        sums_h, _ = one_step(args.steps - 1, solver_h)
+        one_step(args.steps - 1, solver_h)
+        sums_h = solver_h.last_point_sums
 
     if rank == 0:
         value = total_steps / max_elapsed
         fps = perfmodel.flops_per_step(sc)
-        # dominant kernel: wost_walk_kernel<NEU,SRC,DELTA> on this rank (HIP events on its stream)
+        # dominant kernel: the walk kernel on this rank (HIP events on libwost's stream)
         ach_tflops = fps * steps_local / (kernel_ms * 1e-3) / 1e12
-        bytes_per_launch = perfmodel.hbm_bytes_per_walk() * (len(sc.points) * W)
+        bytes_per_launch = perfmodel.hbm_bytes_per_walk() * (len(sc.points) * (w1 - w0))
         ach_gbs = bytes_per_launch * launches / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
-        Wt = W * world   # walks per electrode of the whole job
-        mean = sums[:, 0] / Wt
+        mean = last_sums[:, 0] / Wt
         out = {
             "metric": "walk-steps/sec",
             "value": value,
@@ -308,15 +303,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * max_elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference DCR scenario fields/geometry, Philox4x32-10 walks)",
             "config": {"workload": "dcr_dipole (testGeophysicalScenario fields, eps=0.9, maxSteps=500)",
-                       "electrodes": len(sc.points), "walks_per_electrode": Wt, "walks_per_electrode_per_gpu": W,
+                       "electrodes": len(sc.points), "walks_per_electrode": Wt,
+                       "walks_per_electrode_per_gpu": w1 - w0,
                        "walk_steps_per_solve": total_steps // max(args.steps, 1),
-                       "parallelism": f"survey copy per GPU x{world} (distinct walk ids), RCCL all_gather of "
-                                      "block sums"},
+                       "parallelism": (f"walk-range shards of every electrode over {world} GPUs "
+                                       "(wost_solve_distributed: libwost RCCL all-gather of block sums)")
+                       if world > 1 else "one GPU"},
             "roofline": {"bound": "valu", "achieved": ach_tflops, "peak": perfmodel.FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": ach_tflops / perfmodel.FP32_PEAK_TFLOPS, "traffic": None,
                          "model_flops_per_step": fps, "flop_model": "SURVEY.md 8(d) v1 per-config total (C4 ~350)",
@@ -346,13 +343,14 @@ def main():
         else:
             out["cpu_baseline"] = None
         if not args.no_rho:
-            st_m, st_h = stats_from_sums(sums, Wt), stats_from_sums(sums_h, Wt)
+            st_m, st_h = stats_from_sums(last_sums, Wt), stats_from_sums(sums_h, Wt)
             gpu_full = ((st_m.mean, st_m.stderr), (st_h.mean, st_h.stderr), Wt)
             paired = paired_walks(survey, sc, solver, solver_h, RHO_REPLICA_WALKS * RHO_REPLICAS)
             out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu, paired)
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.barrier()
+        comm.close()
 
 
 if __name__ == "__main__":

@@ -8,9 +8,9 @@ global block order: the result is bitwise that of a one-GPU solve for any R
 (SURVEY.md 8e). The reference has no parallel code.
 
 The only thing libwost needs from outside is the 128-byte RCCL unique id, made on one
-rank and handed to the others: ``Communicator.from_torch`` uses an initialised
-torch.distributed group (gloo is enough -- it carries only these bytes),
-``Communicator.from_file`` a file that every rank can read.
+rank and handed to the others: ``Communicator.from_env`` uses the launcher's TCP
+store (torchrun's MASTER_ADDR/MASTER_PORT; no process group), ``from_torch`` an
+initialised torch.distributed group, ``from_file`` a file every rank can read.
 """
 from __future__ import annotations
 
@@ -28,6 +28,26 @@ def shard_walk_range(walks_per_point: int, n_ranks: int, rank: int) -> tuple[int
     nb = (int(walks_per_point) + _lib.WOST_BLOCK_WALKS - 1) // _lib.WOST_BLOCK_WALKS
     b0, b1 = nb * rank // n_ranks, nb * (rank + 1) // n_ranks
     return min(b0 * _lib.WOST_BLOCK_WALKS, walks_per_point), min(b1 * _lib.WOST_BLOCK_WALKS, walks_per_point)
+
+
+def exchange_over_store(make_id, key: str = "wost_comm_uid", timeout: float = 300.0):
+    """Rank 0 publishes make_id() under `key` in the TCP store at MASTER_ADDR:MASTER_PORT,
+    every rank reads it back: (bytes, store). Under torchrun's elastic agent the store
+    already listens on MASTER_PORT (TORCHELASTIC_USE_AGENT_STORE) and every rank joins
+    it as a client; otherwise rank 0 hosts it. The key is scoped by the run id and
+    restart count, so a restarted job never reads a stale id."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
+                          is_master=(rank == 0 and not agent), timeout=timedelta(seconds=timeout))
+    k = f"{key}/{os.environ.get('TORCHELASTIC_RUN_ID', '')}/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+    if rank == 0:
+        store.set(k, make_id())
+    return bytes(store.get(k)), store
 
 
 def unique_id() -> bytes:
@@ -60,6 +80,21 @@ class Communicator:
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         return cls(box[0], world, rank, device)
+
+    @classmethod
+    def from_env(cls, device: int | None = None, key: str = "wost_comm_uid", timeout: float = 300.0) -> "Communicator":
+        """Bootstrap from the torchrun environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR,
+        MASTER_PORT) without a torch process group: the id travels through a TCP
+        key-value store (exchange_over_store)."""
+        rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        if world == 1:
+            return cls(unique_id(), 1, 0, device)
+        uid, store = exchange_over_store(unique_id, key, timeout)
+        c = cls(uid, world, rank, device)
+        c._store = store   # keep the store (and, on rank 0, its server) alive with the communicator
+        return c
 
     @classmethod
     def from_file(cls, path: str, n_ranks: int, rank: int, device: int, timeout: float = 120.0) -> "Communicator":
@@ -129,5 +164,6 @@ def solve_distributed(solver, comm: Communicator, points, nWalks: int, maxSteps:
     timing = {k: getattr(t.local, k) for k, _ in _lib.WostTiming._fields_}
     timing.update({"walk_begin": int(t.walk_begin), "walk_end": int(t.walk_end), "all_steps": int(t.total_steps)})
     solver.last_timing = timing
+    solver.last_point_sums = sums
     st = stats_from_sums(sums[:, [0, 1, -1]] if sums.shape[1] > 3 else sums, int(nWalks))
     return st.mean.astype(np.float32).reshape(n, 1), st, timing

@@ -929,13 +929,62 @@ int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
 int wost_solve_range(wost_handle* h, const float* points, int64_t n_points, int64_t W, int64_t walk_begin,
                      int64_t walk_end, int32_t max_steps, float eps, uint64_t seed, double* block_stats,
                      double* point_stats, float* walk_values, uint32_t* walk_steps) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
     if (walk_begin == 0 && walk_end == W) {   // the whole range: an ordinary solve
         const int64_t nb = wost_num_blocks(n_points, W);
         return solve_impl(h, points, n_points, W, 0, nb, max_steps, eps, seed, block_stats, point_stats,
                           walk_values, walk_steps, nullptr, true);
     }
-    return solve_impl(h, points, n_points, W, 0, 0, max_steps, eps, seed, block_stats, point_stats, walk_values,
-                      walk_steps, nullptr, true, walk_begin, walk_end);
+    const int ns = h->n_sources;
+    const int64_t chunk = (kMaxBatchWalks / ns) / WOST_BLOCK_WALKS * WOST_BLOCK_WALKS;   // walks of a point per launch
+    if (walk_end - walk_begin <= chunk || walk_begin < 0 || walk_end <= walk_begin || n_points <= 0)
+        return solve_impl(h, points, n_points, W, 0, 0, max_steps, eps, seed, block_stats, point_stats, walk_values,
+                          walk_steps, nullptr, true, walk_begin, walk_end);
+    // a range longer than one launch holds per point: block-aligned sub-ranges, one solve
+    // each, scattered into the range's layout; point sums in the range's block order
+    const int row = 2 * ns + 1;
+    const int64_t Wr = walk_end - walk_begin;
+    const int64_t nbr = (Wr + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
+    std::vector<double> all((size_t)n_points * nbr * row);
+    std::vector<double> part;
+    std::vector<float> pv;
+    std::vector<uint32_t> ps;
+    wost_timing acc{};
+    for (int64_t c0 = walk_begin; c0 < walk_end; c0 += chunk) {
+        const int64_t c1 = std::min(walk_end, c0 + chunk);
+        const int64_t wc = c1 - c0, nbc = (wc + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
+        const int64_t boff = (c0 - walk_begin) / WOST_BLOCK_WALKS, woff = c0 - walk_begin;
+        part.resize((size_t)n_points * nbc * row);
+        if (walk_values) pv.resize((size_t)n_points * wc * ns);
+        if (walk_steps) ps.resize((size_t)n_points * wc);
+        int rc = solve_impl(h, points, n_points, W, 0, 0, max_steps, eps, seed, part.data(), nullptr,
+                            walk_values ? pv.data() : nullptr, walk_steps ? ps.data() : nullptr, nullptr, true, c0, c1);
+        if (rc != WOST_OK) return rc;
+        for (int64_t p = 0; p < n_points; ++p) {
+            std::memcpy(&all[((size_t)p * nbr + boff) * row], &part[(size_t)p * nbc * row], sizeof(double) * nbc * row);
+            if (walk_values)
+                std::memcpy(walk_values + ((size_t)p * Wr + woff) * ns, &pv[(size_t)p * wc * ns], sizeof(float) * wc * ns);
+            if (walk_steps) std::memcpy(walk_steps + (size_t)p * Wr + woff, &ps[(size_t)p * wc], sizeof(uint32_t) * wc);
+        }
+        acc.walk_kernel_ms += h->timing.walk_kernel_ms;
+        acc.reduce_kernel_ms += h->timing.reduce_kernel_ms;
+        acc.total_ms += h->timing.total_ms;
+        acc.n_launches += h->timing.n_launches;
+        acc.total_steps += h->timing.total_steps;
+        acc.total_walks += h->timing.total_walks;
+        acc.grid_blocks = h->timing.grid_blocks;
+        acc.jit = h->timing.jit;
+        acc.tree = h->timing.tree;
+    }
+    if (block_stats) std::memcpy(block_stats, all.data(), sizeof(double) * all.size());
+    if (point_stats) {
+        std::fill(point_stats, point_stats + (size_t)row * n_points, 0.0);
+        for (int64_t p = 0; p < n_points; ++p)
+            for (int64_t b = 0; b < nbr; ++b)
+                for (int c = 0; c < row; ++c) point_stats[(size_t)row * p + c] += all[((size_t)p * nbr + b) * row + c];
+    }
+    h->timing = acc;
+    return WOST_OK;
 }
 
 int wost_solve_history(wost_handle* h, const float* points, int64_t n_points, int64_t W, int32_t max_steps,

@@ -195,6 +195,7 @@ class WostSolver_2D:
         _lib.check(_lib.lib.wost_get_info(self._h, ctypes.byref(sb), ctypes.byref(dt)), "wost_get_info")
         self.sigma_bar = float(sb.value) if self.use_delta_tracking else None
         self.last_timing = None
+        self.last_point_sums = None   # (sum, sum^2, steps) per point of the last solve
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -261,7 +262,9 @@ class WostSolver_2D:
         p = _points_np(solvePoints)
         n = p.shape[0]
         nbr = -(-(int(walk_end) - int(walk_begin)) // _lib.WOST_BLOCK_WALKS)
-        bs = np.zeros((n, max(nbr, 0), 3), np.float64)
+        ns = ctypes.c_int32(1)
+        _lib.check(_lib.lib.wost_num_sources(self._h, ctypes.byref(ns)), "wost_num_sources")
+        bs = np.zeros((n, max(nbr, 0), 2 * ns.value + 1), np.float64)
         _lib.check(_lib.lib.wost_solve_range(self._h, _lib.fptr(p), n, int(nWalks), int(walk_begin), int(walk_end),
                                              int(maxSteps), float(eps), int(seed) & (2**64 - 1), _lib.dptr(bs), None,
                                              None, None), "WostSolver_2D.solve_range")
@@ -323,6 +326,7 @@ class WostSolver_2D:
                                            int(seed) & (2**64 - 1), None, _lib.dptr(sums), None, None),
                        "WostSolver_2D.solve")
         self.last_timing = self.timing()
+        self.last_point_sums = sums
         u = (sums[:, 0] / nWalks).astype(np.float32).reshape(n, 1)
         out = [_like(u, solvePoints)]
         if return_history:

@@ -262,7 +262,8 @@ int wost_num_sources(const wost_handle* h, int32_t* n_sources);
  *   block_stats [n_points][n_range_blocks][2S+1] (point-major), point_stats
  *   [n_points][2S+1], walk_values [n_points][walk_end - walk_begin][S], walk_steps
  *   [n_points][walk_end - walk_begin]  (S = wost_num_sources).
- * Per point at most 2^26 / S walks (one launch). */
+ * A range longer than one launch holds (2^26 / S walks of a point) is solved as
+ * block-aligned sub-ranges, with the same results. */
 int wost_solve_range(wost_handle* h, const float* points, int64_t n_points,
                      int64_t walks_per_point, int64_t walk_begin, int64_t walk_end,
                      int32_t max_steps, float eps, uint64_t seed,

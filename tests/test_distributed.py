@@ -161,3 +161,43 @@ def test_walk_range_shards_match_the_library():
                 a, b = ctypes.c_int64(), ctypes.c_int64()
                 assert _lib.lib.wost_shard_walk_range(W, R, r, ctypes.byref(a), ctypes.byref(b)) == 0
                 assert (a.value, b.value) == D.shard_walk_range(W, R, r) == comm.shard_walk_range(W, R, r)
+
+
+# ---------------------------------------------------------------- communicator bootstrap
+def _store_worker(rank, world, port, agent, out_q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from dcrmontecarlo_amd import comm
+
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      TORCHELASTIC_RUN_ID="t1", TORCHELASTIC_USE_AGENT_STORE="True" if agent else "False")
+    uid, store = comm.exchange_over_store(lambda: bytes(range(128)) if rank == 0 else b"wrong", timeout=60)
+    out_q.put((rank, uid))
+    store.set(f"done{rank}", b"1")
+    if rank == 0 and not agent:   # the host of the store outlives every reader
+        for r in range(world):
+            store.get(f"done{r}")
+
+
+@pytest.mark.parametrize("agent", [False, True])
+def test_communicator_id_travels_through_the_launch_store(agent):
+    """Communicator.from_env's id exchange (the part that needs no GPU): rank 0's 128 bytes
+    reach every rank, with rank 0 hosting the store or torchrun's agent hosting it."""
+    from datetime import timedelta
+
+    world = 3
+    port = _free_port()
+    host = dist.TCPStore("127.0.0.1", port, None, is_master=True, timeout=timedelta(seconds=60),
+                         wait_for_workers=False) if agent else None
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_store_worker, args=(r, world, port, agent, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res[r] == bytes(range(128)) for r in range(world))
+    del host
