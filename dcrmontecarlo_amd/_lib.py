@@ -115,6 +115,8 @@ def _load():
         "wost_solve_distributed": (c_int32, [H, c_void_p, POINTER(c_float), c_int64, c_int64, c_int32, c_float,
                                              c_uint64, POINTER(c_double), POINTER(WostDistTiming)]),
         "wost_greens_norm": (c_int32, [c_double, POINTER(c_float), c_int64, POINTER(c_float)]),
+        "wost_screened_sample_fixed": (c_int32, [POINTER(c_float), POINTER(c_float), c_int64, POINTER(c_float)]),
+        "wost_screened_cdf_fixed": (c_int32, [c_double, POINTER(c_double), c_int64, POINTER(c_double)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
         "wost_kernel_source": (c_int32, [POINTER(WostProblem), ctypes.c_char_p, c_int64, POINTER(c_int64)]),

@@ -275,12 +275,30 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
     return fn;
 }
 
+// The corrected screened sampler's nodes do not depend on sigma_bar (only on the
+// shape s = R sqrt(sigma_bar)): built once per process (~0.5 s of Bessel series).
+const std::vector<float>& fixed_screened_table() {
+    static const std::vector<float> t = [] {
+        std::vector<float> v((size_t)kFixTableFloats);
+        screened_fixed_nodes(v.data(), kFixRows, kFixCols, kFixXMax);
+        return v;
+    }();
+    return t;
+}
+
 int ensure_table(wost_handle* h) {
     if (h->table_ready) return WOST_OK;
-    // sampler nodes, then (delta tracking) the G_norm cells (wost_device.h)
-    const size_t n = table_floats(h->delta);
+    // sampler nodes, then (delta tracking) the G_norm cells (wost_device.h), then
+    // (compat="fixed" delta tracking) the corrected screened sampler's nodes
+    const bool fix_delta = h->delta && h->compat == WOST_COMPAT_FIXED;
+    const size_t n = table_floats(h->delta, fix_delta);
     h->table.assign(n, 0.f);
-    if (h->delta) {
+    if (fix_delta) {
+        greens_sampler_nodes_jacobian(h->table.data(), WOST_SAMPLER_TABLE_N);   // staged, unused
+        greens_norm_cells(h->table.data() + kSamplerFloatsPadded, kGnormCells, (double)kGnormCells / kGnormInvH);
+        const std::vector<float>& fx = fixed_screened_table();
+        std::memcpy(h->table.data() + kFixTableOffset, fx.data(), sizeof(float) * fx.size());
+    } else if (h->delta) {
         screened_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N, h->sigma_bar);
         greens_norm_cells(h->table.data() + kSamplerFloatsPadded, kGnormCells, (double)kGnormCells / kGnormInvH);
     } else if (h->compat == WOST_COMPAT_FIXED) {
@@ -288,7 +306,7 @@ int ensure_table(wost_handle* h) {
     } else {
         greens_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N);
     }
-    if (!h->d_table) HIP_TRY(hipMalloc(&h->d_table, sizeof(float) * table_floats(true)));
+    if (!h->d_table) HIP_TRY(hipMalloc(&h->d_table, sizeof(float) * std::max(n, table_floats(true))));
     HIP_TRY(hipMemcpy(h->d_table, h->table.data(), sizeof(float) * n, hipMemcpyHostToDevice));
     h->table_ready = true;
     return WOST_OK;
@@ -377,8 +395,10 @@ bool use_tree(const wost_handle* h) {
 int walk_mode(const wost_handle* h) {
     const bool neu = !h->nverts.empty();
     const bool src = h->fields[SLOT_F].present;
-    if (h->compat == WOST_COMPAT_FIXED)   // scan queries (no segment tree)
+    if (h->compat == WOST_COMPAT_FIXED) {   // scan queries (no segment tree)
+        if (h->delta) return neu ? MODE_FIX_MIXED_DELTA : MODE_FIX_DELTA;
         return neu ? (src ? MODE_FIX_MIXED_POISSON : MODE_FIX_MIXED) : (src ? MODE_FIX_POISSON : MODE_FIX_DIRICHLET);
+    }
     const bool tree = neu && use_tree(h);
     if (h->delta) return neu ? (tree ? MODE_MIXED_DELTA_TREE : MODE_MIXED_DELTA) : MODE_DELTA;
     if (neu) return src ? (tree ? MODE_MIXED_POISSON_TREE : MODE_MIXED_POISSON) : (tree ? MODE_MIXED_TREE : MODE_MIXED);
@@ -489,10 +509,6 @@ int create_host(const wost_problem* pb, wost_handle** out) {
     *out = nullptr;
     if (pb->compat != WOST_COMPAT_REFERENCE && pb->compat != WOST_COMPAT_FIXED)
         return fail(WOST_ERR_INVALID_ARG, "unknown compat %d", pb->compat);
-    if (pb->compat == WOST_COMPAT_FIXED && (pb->sigma || pb->alpha))
-        return fail(WOST_ERR_UNSUPPORTED,
-                    "compat='fixed' covers the Laplace, Poisson and mixed estimators; delta tracking (sigma/alpha, "
-                    "quirks Q4/Q5) runs with compat='reference' only");
     wost_handle* h = new wost_handle();
     h->device = -1;
     int rc;
@@ -644,6 +660,19 @@ int wost_greens_norm(double sigma_bar, const float* radii, int64_t n, float* out
         const float r = radii[i];
         out[i] = greens_norm_from_table(cells.data(), r * sqrt_sb, r, inv_sb);
     }
+    return WOST_OK;
+}
+
+int wost_screened_sample_fixed(const float* s, const float* u, int64_t n, float* rho) {
+    if (n < 0 || (n > 0 && (!s || !u || !rho))) return fail(WOST_ERR_INVALID_ARG, "need n >= 0 and buffers");
+    const std::vector<float>& t = fixed_screened_table();
+    for (int64_t i = 0; i < n; ++i) rho[i] = sample_rho_screened_fixed(t.data(), u[i], s[i]);
+    return WOST_OK;
+}
+
+int wost_screened_cdf_fixed(double s, const double* rho, int64_t n, double* cdf) {
+    if (!(s >= 0.0) || n < 0 || (n > 0 && (!rho || !cdf))) return fail(WOST_ERR_INVALID_ARG, "need s >= 0, n >= 0");
+    for (int64_t i = 0; i < n; ++i) cdf[i] = screened_fixed_cdf(rho[i], s);
     return WOST_OK;
 }
 

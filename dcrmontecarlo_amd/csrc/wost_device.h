@@ -100,6 +100,7 @@ WOST_HD float f_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 WOST_HD float f_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
 WOST_HD float f_sin(float x) { return __sinf(x); }
 WOST_HD float f_cos(float x) { return __cosf(x); }
+WOST_HD float f_log(float x) { return __logf(x); }
 #else
 WOST_HD float f_exp(float x) { return expf(x); }
 WOST_HD float f_rcp(float x) { return 1.0f / x; }
@@ -108,6 +109,7 @@ WOST_HD float f_sqrt(float x) { return sqrtf(x); }
 WOST_HD float f_rsq(float x) { return 1.0f / sqrtf(x); }
 WOST_HD float f_sin(float x) { return sinf(x); }
 WOST_HD float f_cos(float x) { return cosf(x); }
+WOST_HD float f_log(float x) { return logf(x); }
 #endif
 
 // ---------------------------------------------------------------------------
@@ -559,6 +561,46 @@ WOST_HD float sample_rho_tail(const float* tail, float node0, float u) {
     float a = q[0], b = q[1];
     a = i == 0 ? node0 : a;
     return a + f * (b - a);
+}
+
+// compat="fixed" screened sampler (quirks Q4/Q5 corrected; wost_tables.cpp
+// screened_fixed_nodes): the radius of a point drawn from the ball's screened
+// Green's function, as a fraction rho of the ball radius R, for the shape s =
+// R sqrt(sigma_bar). The [kFixRows][kFixCols] table holds inverse-CDF nodes of
+// rows s_j = expm1(j dx) (row 0: the Laplace law) at quantiles u(v) = 2v^2 /
+// 1 - 2(1-v)^2 of a uniform v grid; the sample interpolates linearly in v and
+// in x = ln(1+s). Beyond the last row (s > 40: c = K0(s)/I0(s) and the law's
+// mass beyond rho = 1 are below 1e-15) the law is s-invariant in t = rho s, so
+// the last row is rescaled by s_max / s.
+// ---------------------------------------------------------------------------
+constexpr int kFixRows = 129;
+constexpr int kFixCols = 257;
+constexpr float kFixSMax = 40.0f;
+constexpr double kFixXMax = 3.7135720667043078;   // ln(1 + kFixSMax)
+constexpr int kFixTableFloats = kFixRows * kFixCols;
+constexpr int kFixTableOffset = kSamplerFloatsPadded + 4 * kGnormCells;   // in WalkArgs::table
+
+template <class TabP>
+WOST_HD float sample_rho_screened_fixed(TabP tab, float u, float s) {
+    // quantile -> v: inverse of u = 2 v^2 (v < 1/2), 1 - 2 (1 - v)^2
+    const float v = u < 0.5f ? f_sqrt(0.5f * u) : 1.0f - f_sqrt(0.5f - 0.5f * u);
+    float pv = v * (float)(kFixCols - 1);
+    pv = pv < 0.0f ? 0.0f : pv;
+    int i = (int)pv;
+    i = i > kFixCols - 2 ? kFixCols - 2 : i;
+    const float fv = pv - (float)i;
+    const float px = f_log(1.0f + s) * (float)((kFixRows - 1) / kFixXMax);
+    int j = (int)px;
+    float lam = px - (float)j, scale = 1.0f;
+    if (!(j < kFixRows - 1)) {   // s > s_max (or not finite): the t-invariant tail
+        j = kFixRows - 2;
+        lam = 1.0f;
+        scale = f_div(kFixSMax, s);
+    }
+    const int o = j * kFixCols + i;
+    const float a0 = tab[o], a1 = tab[o + 1], b0 = tab[o + kFixCols], b1 = tab[o + kFixCols + 1];
+    const float a = a0 + fv * (a1 - a0), b = b0 + fv * (b1 - b0);
+    return (a + lam * (b - a)) * scale;
 }
 
 // ---------------------------------------------------------------------------

@@ -25,21 +25,27 @@ enum WalkMode : int {
     MODE_FIX_DIRICHLET = 9,
     MODE_FIX_POISSON = 10,
     MODE_FIX_MIXED = 11,
-    MODE_FIX_MIXED_POISSON = 12
+    MODE_FIX_MIXED_POISSON = 12,
+    // compat="fixed" delta tracking (Q4/Q5 corrected sampler), Dirichlet only / + Neumann
+    MODE_FIX_DELTA = 13,
+    MODE_FIX_MIXED_DELTA = 14
 };
 
-inline bool mode_fix(int m) { return m >= MODE_FIX_DIRICHLET && m <= MODE_FIX_MIXED_POISSON; }
+inline bool mode_fix(int m) { return m >= MODE_FIX_DIRICHLET && m <= MODE_FIX_MIXED_DELTA; }
 inline bool mode_tree(int m) { return m >= MODE_MIXED_TREE && m <= MODE_MIXED_DELTA_TREE; }
 inline bool mode_neu(int m) {
     return m == MODE_MIXED || m == MODE_MIXED_POISSON || m == MODE_MIXED_DELTA || mode_tree(m) ||
-           m == MODE_FIX_MIXED || m == MODE_FIX_MIXED_POISSON;
+           m == MODE_FIX_MIXED || m == MODE_FIX_MIXED_POISSON || m == MODE_FIX_MIXED_DELTA;
 }
 inline bool mode_src(int m) {
     return m == MODE_POISSON || m == MODE_MIXED_POISSON || m == MODE_DELTA || m == MODE_MIXED_DELTA ||
            m == MODE_MIXED_POISSON_TREE || m == MODE_MIXED_DELTA_TREE || m == MODE_FIX_POISSON ||
-           m == MODE_FIX_MIXED_POISSON;
+           m == MODE_FIX_MIXED_POISSON || m == MODE_FIX_DELTA || m == MODE_FIX_MIXED_DELTA;
 }
-inline bool mode_delta(int m) { return m == MODE_DELTA || m == MODE_MIXED_DELTA || m == MODE_MIXED_DELTA_TREE; }
+inline bool mode_delta(int m) {
+    return m == MODE_DELTA || m == MODE_MIXED_DELTA || m == MODE_MIXED_DELTA_TREE || m == MODE_FIX_DELTA ||
+           m == MODE_FIX_MIXED_DELTA;
+}
 
 // const_d / const_n: the kernel has the Dirichlet / Neumann polyline compiled in
 // (field-specialised kernels, wost_jit.cpp), so it stages no copy.
@@ -48,10 +54,13 @@ inline size_t walk_lds_bytes(int mode, int nd, int nn, int n_points, int tree_ld
     return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points, mode_tree(mode), mode_delta(mode),
                               tree_lds, const_d, const_n && !mode_fix(mode));
 }
-// floats of the sampler / G_norm table buffer (WalkArgs::table)
-inline size_t table_floats(bool delta) {
-    return (size_t)kSamplerFloatsPadded + (delta ? 4 * (size_t)kGnormCells : 0);
+// floats of the sampler / G_norm table buffer (WalkArgs::table); compat="fixed" delta
+// tracking appends the corrected screened sampler's [kFixRows][kFixCols] nodes
+inline size_t table_floats(bool delta, bool fixed_delta = false) {
+    return (size_t)kSamplerFloatsPadded + (delta ? 4 * (size_t)kGnormCells : 0) +
+           (fixed_delta ? (size_t)kFixTableFloats : 0);
 }
+
 
 // precompiled (interpreted-field) walk kernels
 hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu);

@@ -225,6 +225,21 @@ struct Entry {
 std::mutex g_mu;
 std::map<std::string, Entry> g_modules;   // key: device:arch:hash
 
+// hiprtc options besides --offload-arch. They change the code's FP semantics, so they
+// are part of the cache key (cache_identity), as are the compiler and runtime versions.
+const char* const kCompileOptions[] = {"-O3", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt",
+                                       "-ffp-contract=fast-honor-pragmas"};
+constexpr int kCacheFormat = 2;   // bump when the generator or the cached file layout changes
+
+std::string cache_identity() {
+    std::string id = "fmt" + std::to_string(kCacheFormat);
+    for (const char* o : kCompileOptions) id += std::string("|") + o;
+    int maj = 0, min = 0, rt = 0;
+    if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) id += "|hiprtc" + std::to_string(maj) + "." + std::to_string(min);
+    if (hipRuntimeGetVersion(&rt) == hipSuccess) id += "|hip" + std::to_string(rt);
+    return id;
+}
+
 bool compile(const std::string& src, const std::string& arch, std::vector<char>& code, std::string* err) {
     const char* hdrs[] = {wost_embedded_wost_h, wost_embedded_wost_device_h, wost_embedded_wost_walk_h};
     const char* names[] = {"wost.h", "wost_device.h", "wost_walk.h"};
@@ -234,9 +249,9 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
         return false;
     }
     std::string arch_opt = "--offload-arch=" + arch;
-    const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt",
-                          "-ffp-contract=fast-honor-pragmas"};
-    hiprtcResult rc = hiprtcCompileProgram(prog, 5, opts);
+    std::vector<const char*> opts = {arch_opt.c_str()};
+    for (const char* o : kCompileOptions) opts.push_back(o);
+    hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -386,9 +401,11 @@ bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, st
     }
     std::string arch = prop.gcnArchName;
     arch = arch.substr(0, arch.find(':'));
-    // the embedded headers are part of the key: a rebuilt library never reuses stale code
-    const uint64_t h = fnv1a(source + "|" + arch + "|" + wost_embedded_wost_h + wost_embedded_wost_device_h +
-                             wost_embedded_wost_walk_h);
+    // the embedded headers, compile options and compiler/runtime versions are part of the
+    // key: a rebuilt library, other options or a ROCm upgrade never reuse stale code
+    static const std::string ident = cache_identity();
+    const uint64_t h = fnv1a(source + "|" + arch + "|" + ident + "|" + wost_embedded_wost_h +
+                             wost_embedded_wost_device_h + wost_embedded_wost_walk_h);
     char hex[32];
     std::snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)h);
     const std::string key = std::to_string(device) + ":" + arch + ":" + hex;

@@ -149,6 +149,8 @@ wost_walk_kernel(const WalkArgs A) {
     case MODE_FIX_POISSON: X(false, true, false, false, true);        \
     case MODE_FIX_MIXED: X(true, false, false, false, true);          \
     case MODE_FIX_MIXED_POISSON: X(true, true, false, false, true);   \
+    case MODE_FIX_DELTA: X(false, true, true, false, true);           \
+    case MODE_FIX_MIXED_DELTA: X(true, true, true, false, true);      \
     default: return hipErrorInvalidValue;                        \
     }
 

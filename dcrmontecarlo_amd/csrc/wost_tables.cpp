@@ -195,4 +195,133 @@ void screened_sampler_nodes(float* out, int n, double sigma_bar) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// compat="fixed" screened sampler (quirks Q4/Q5 corrected). A point y sampled
+// from the ball's screened Green's function G(x, y; R) (2-D, sigma_bar) has
+// radius rho R with, for the shape parameter s = R sqrt(sigma_bar),
+//   p_s(rho) ~ rho [K0(rho s) - c I0(rho s)],  c = K0(s) / I0(s),
+// whose CDF is closed-form (d/dt[-t K1(t)] = t K0(t), d/dt[t I1(t)] = t I0(t),
+// and the Wronskian I0 K1 + I1 K0 = 1/s for the normaliser):
+//   F_s(rho) = (1 - t K1(t) - c t I1(t)) / (1 - 1/I0(s)),  t = rho s.
+// s -> 0 gives the Laplace law rho^2 (1 + 2 ln(1/rho)).
+// ---------------------------------------------------------------------------
+static void bessel_i01(double t, double* i0, double* i1) {
+    // power series; every term is positive (no cancellation) and t <= kFixSMax
+    const double q = 0.25 * t * t;
+    double a = 1.0, b = 0.5 * t, s0 = a, s1 = b;
+    for (int k = 1; k < 400; ++k) {
+        a *= q / ((double)k * k);
+        b *= q / ((double)k * (k + 1));
+        s0 += a;
+        s1 += b;
+        if (a <= 1e-18 * s0 && b <= 1e-18 * s1) break;
+    }
+    *i0 = s0;
+    *i1 = s1;
+}
+
+static void bessel_k01(double t, double* k0, double* k1) {
+    if (t <= 2.0) {
+        // A&S 9.6.13 / 9.6.11: K0 = -(ln(t/2) + gamma) I0 + sum q^k/(k!)^2 H_k,
+        // K1 = 1/t + ln(t/2) I1 - (t/4) sum (psi(k+1) + psi(k+2)) q^k / (k! (k+1)!)
+        const double gamma = 0.57721566490153286061;
+        double i0, i1;
+        bessel_i01(t, &i0, &i1);
+        const double q = 0.25 * t * t;
+        double a = 1.0, b = 1.0, hk = 0.0, s0 = 0.0, s1 = 0.0;
+        s1 = (-gamma + (-gamma + 1.0)) * b;                 // k = 0: psi(1) + psi(2)
+        for (int k = 1; k < 60; ++k) {
+            a *= q / ((double)k * k);
+            b *= q / ((double)k * (k + 1));
+            hk += 1.0 / k;
+            s0 += a * hk;
+            s1 += b * ((-gamma + hk) + (-gamma + hk + 1.0 / (k + 1)));
+        }
+        *k0 = -(std::log(0.5 * t) + gamma) * i0 + s0;
+        *k1 = 1.0 / t + std::log(0.5 * t) * i1 - 0.25 * t * s1;
+        return;
+    }
+    // K_nu(t) = int_0^inf exp(-t cosh u) cosh(nu u) du: trapezoid, spectrally accurate
+    const double h = 0.05;
+    double a0 = 0.5 * std::exp(-t), a1 = a0;
+    for (int j = 1;; ++j) {
+        const double u = j * h, e = std::exp(-t * std::cosh(u));
+        a0 += e;
+        a1 += e * std::cosh(u);
+        if (e < 1e-300 || e * std::cosh(u) < 1e-18 * a1) break;
+    }
+    *k0 = a0 * h;
+    *k1 = a1 * h;
+}
+
+// F_s and its density dF/drho at rho, with the row constants c = K0(s)/I0(s) and
+// den = 1 - 1/I0(s) precomputed.
+struct ScreenedRow {
+    double s = 0.0, c = 0.0, den = 1.0;
+    explicit ScreenedRow(double s_) : s(s_) {
+        if (s <= 0.0) return;
+        double k0s, k1s, i0s, i1s;
+        bessel_k01(s, &k0s, &k1s);
+        bessel_i01(s, &i0s, &i1s);
+        c = k0s / i0s;
+        den = 1.0 - 1.0 / i0s;
+    }
+    void eval(double rho, double* F, double* p) const {
+        if (!(rho > 0.0)) { *F = 0.0; *p = 0.0; return; }
+        if (s <= 0.0) {
+            const double l = -std::log(rho);
+            *F = rho * rho * (1.0 + 2.0 * l);
+            *p = 4.0 * rho * l;
+            return;
+        }
+        const double t = rho * s;
+        double k0t, k1t, i0t, i1t;
+        bessel_k01(t, &k0t, &k1t);
+        bessel_i01(t, &i0t, &i1t);
+        *F = (1.0 - t * k1t - c * t * i1t) / den;
+        *p = s * t * (k0t - c * i0t) / den;
+    }
+};
+
+double screened_fixed_cdf(double rho, double s) {
+    if (!(rho > 0.0)) return 0.0;
+    if (rho >= 1.0) return 1.0;
+    double F, p;
+    ScreenedRow(s).eval(rho, &F, &p);
+    return std::min(1.0, std::max(0.0, F));
+}
+
+double screened_fixed_node_u(int i, int cols) {
+    const double v = (double)i / (double)(cols - 1);
+    return v < 0.5 ? 2.0 * v * v : 1.0 - 2.0 * (1.0 - v) * (1.0 - v);
+}
+
+void screened_fixed_nodes(float* out, int rows, int cols, double xmax) {
+    for (int j = 0; j < rows; ++j) {
+        const ScreenedRow row_law(j == 0 ? 0.0 : std::expm1(xmax * (double)j / (double)(rows - 1)));
+        float* row = out + (size_t)j * cols;
+        row[0] = 0.0f;
+        row[cols - 1] = 1.0f;
+        double lo0 = 0.0, x = 0.5;   // targets increase along the row: brackets and guesses carry over
+        for (int i = 1; i < cols - 1; ++i) {
+            const double u = screened_fixed_node_u(i, cols);
+            double lo = lo0, hi = 1.0;
+            x = std::min(std::max(x, lo), hi);
+            if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+            // safeguarded Newton: a step that leaves the bracket is replaced by bisection
+            for (int it = 0; it < 100; ++it) {
+                double F, p;
+                row_law.eval(x, &F, &p);
+                if (F < u) lo = x; else hi = x;
+                const double xn = p > 0.0 ? x - (F - u) / p : -1.0;
+                const double next = (xn > lo && xn < hi) ? xn : 0.5 * (lo + hi);
+                if (std::fabs(next - x) <= 1e-15 * x || hi - lo <= 1e-16) { x = next; break; }
+                x = next;
+            }
+            lo0 = lo;
+            row[i] = (float)x;
+        }
+    }
+}
+
 }  // namespace wost

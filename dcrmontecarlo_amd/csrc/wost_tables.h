@@ -44,4 +44,16 @@ void greens_sampler_nodes(float* out, int n);
 void greens_sampler_nodes_jacobian(float* out, int n);
 void screened_sampler_nodes(float* out, int n, double sigma_bar);
 
+// compat="fixed" screened sampler (Q4/Q5 corrected): the exact radial law of a
+// point sampled from the ball's screened Green's function, CDF F_s(rho) for the
+// shape parameter s = R sqrt(sigma_bar) (closed form in I0, I1, K0, K1; s = 0: the
+// Laplace law). screened_fixed_nodes fills [rows][cols] inverse-CDF nodes: row j
+// is s_j = expm1(xmax j / (rows-1)) (row 0: s = 0), column i the quantile
+// u_i = screened_fixed_node_u(i, cols) = 2 v^2 (v < 1/2) or 1 - 2 (1-v)^2, v =
+// i / (cols-1), so that the steep ends of the inverse CDF are resolved
+// (wost_device.h sample_rho_screened_fixed).
+double screened_fixed_cdf(double rho, double s);
+double screened_fixed_node_u(int i, int cols);
+void screened_fixed_nodes(float* out, int rows, int cols, double xmax);
+
 }  // namespace wost

@@ -107,8 +107,8 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // source's total is bit for bit what a single-source solve of it gives. The
 // Fields policy then provides f_multi(x, y, float out[NS]); per-walk values go
 // to out_val[local walk * NS + k].
-// FIX (compat="fixed", Laplace / Poisson / mixed): the estimator with the
-// reference's quirks corrected:
+// FIX (compat="fixed"): the estimator with the reference's quirks corrected
+// (SURVEY 8a):
 //  Q7/Q12 the walk stops when the CURRENT point's Dirichlet distance is <= eps
 //         (no extra step inside the eps-shell; eps >= 1 no longer skips walks);
 //  Q1     the Neumann ray query takes the nearest crossing along the ray;
@@ -116,15 +116,34 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 //         INWARD normal (the side the ray came from);
 //  Q3     the source radius follows the Green's density with its Jacobian,
 //         rho ln(1/rho) (the host builds that sampler table);
-//  Q13    the source sample takes its own direction (Philox word w) and counts
-//         only if it is visible from x (no Neumann crossing before it).
+//  Q13    (Laplace / Poisson / mixed) the source sample takes its own direction
+//         (Philox word w) and counts only if it is visible from x (no Neumann
+//         crossing before it); on a Neumann boundary point that direction, like
+//         the step's, is uniform on the inward hemisphere (the star-shaped region
+//         is then a half-ball: the full ball's radial law over a half-circle of
+//         directions gives the factor 2 of the boundary representation);
+//  Q4/Q5  delta tracking draws the sample from the ball's screened Green's
+//         function of THIS radius (shape s = R sqrt(sigma_bar), Jacobian
+//         included, no clipped envelope; sample_rho_screened_fixed).
+//  Delta tracking with Neumann boundaries needs more than the reference's
+//  collision rule: along a ray that meets the boundary at distance d < R, the
+//  screened Poisson kernel's weight there is t (K1(t) + c I1(t)) (t = d
+//  sqrt(sigma_bar)), not 1/I0(R sqrt(sigma_bar)) -- per direction, the
+//  no-collision probability must be 1 - sigma_bar |G| F_s(d / R). FIX draws the
+//  sample on the step's ray and collides only when mu <= sigma_bar |G| AND the
+//  sample lies before the ray's boundary point (probability F_s(d / R)), which is
+//  exactly that, with the collision point from the truncated law; otherwise the
+//  walk moves to the ray's point with weight 1. A collision leaves the Neumann
+//  boundary, and its weight 1 - sigma'/sigma_bar is kept signed (unbiased for
+//  any sigma_bar; the reference's max(., 0) at solvers/WoStSolver.py:282 is
+//  biased wherever sigma' > sigma_bar).
 template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, bool FIX = false, class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
     // the walk's position updates round op by op like the reference (torch CPU
     // has no FMA contraction); the field math it calls keeps its own setting
 #pragma clang fp contract(off)
     static_assert(NS >= 1 && (NS == 1 || SRC) && (NS == 1 || !REC), "multi-source walks need a source, no recorder");
-    static_assert(!(FIX && (DELTA || TREE)), "compat=fixed covers the Laplace, Poisson and mixed scan estimators");
+    static_assert(!(FIX && TREE), "compat=fixed runs the scan queries");
     constexpr bool kStageD = !F::kConstDirichlet;
     constexpr bool kStageN = NEU && !TREE && (!F::kConstNeumann || FIX);   // FIX scans sN itself
     unsigned char* lds = smem;
@@ -283,6 +302,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         // :227-228 (quirk Q2): atan2(normal) is a property of the segment that
         // was hit, precomputed per segment with the same device atan2f
         if (NEU && onB) theta = FIX ? theta / 2.0f + (phi - kPiF / 2.0f) : theta / 2.0f + phi;
+        const bool onB0 = onB;                                       // the current point's, for FIX's
+        const float phi0 = phi;                                      // source direction
         const float cs = f_cos(theta), sn = f_sin(theta);            // :230-232
 
         float xnx, xny;
@@ -309,15 +330,24 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float gnorm = 0.f;
         Jet aj{0.f, 0.f, 0.f, 0.f};
         if (SRC) {                                                   // :242-258
-            const float rs = sample_rho_tail(sT, node0, u01(rn.y)) * r;   // :244 (sampler, quirks Q3-Q5)
-            if constexpr (FIX) {                                     // Q13 fixed: own direction
-                const float ts = (u01(rn.w) * 2.0f) * kPiF;
+            float rs;
+            if constexpr (FIX && DELTA)                              // Q4/Q5 fixed: this ball's law
+                rs = sample_rho_screened_fixed(A.table + kFixTableOffset, u01(rn.y), r * sqrt_sb) * r;
+            else
+                rs = sample_rho_tail(sT, node0, u01(rn.y)) * r;      // :244 (sampler, quirks Q3-Q5)
+            if constexpr (FIX && !DELTA) {                           // Q13 fixed: own direction
+                float ts = (u01(rn.w) * 2.0f) * kPiF;
+                if (NEU && onB0) ts = ts / 2.0f + (phi0 - kPiF / 2.0f);   // the inward hemisphere
                 const float cs2 = f_cos(ts), sn2 = f_sin(ts);
                 yx = px + rs * cs2;
                 yy = py + rs * sn2;
                 if (NEU) clipped = intersect_polylines_ray(sN, A.nn, px, py, cs2, sn2, rs).hit;   // not visible
             } else {
-                yx = px + rs * cs;                                   // :245 (quirk Q13)
+                // :245 (quirk Q13). FIX delta keeps the sample on the step's ray: with the
+                // nearest crossing (Q1) the clip below is exactly "y is in the star-shaped
+                // region", and a collision is taken only there, so it lands at a radius
+                // drawn from the Green's law truncated at the ray's boundary point
+                yx = px + rs * cs;
                 yy = py + rs * sn;
                 const float e1x = yx - px, e1y = yy - py;
                 const float e2x = xnx - px, e2y = xny - py;
@@ -372,7 +402,21 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             rr[1] = float4{yx, yy, cv, SRC ? 1.0f : 0.0f};
         }
 
-        if (DELTA) {                                                 // :271-284
+        if (DELTA && FIX) {
+            const float mu = u01(rn.z);
+            // collision: mu <= sigma_bar |G| and the sample before the ray's boundary point
+            const bool collide = !(mu > sigma_bar * gnorm) && !clipped;
+            float anew = aj.v;                                       // a collision, or a clipped sample (y = z)
+            if (!collide && !clipped) anew = fld.alpha(xnx, xny);
+            float sc = 1.0f;
+            if (collide) sc = 1.0f - sigma_prime_from(aj, fld.sigma(yx, yy), fld.detached()) * inv_sb;
+            const float wt = w * f_sqrt(f_div(anew, ax));
+            w = collide ? wt * sc : wt;
+            px = collide ? yx : xnx;
+            py = collide ? yy : xny;
+            onB = collide ? false : onB;                             // a collision point is interior
+            ax = anew;
+        } else if (DELTA) {                                          // :271-284
             const float mu = u01(rn.z);
             const bool accept = mu > sigma_bar * gnorm;              // :273-275
             // the two branches share the weight update w * sqrt(a_new / alpha(x));

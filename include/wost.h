@@ -60,7 +60,7 @@ enum wost_status {
 
 /* compat: "reference" reproduces the reference's estimator including its
  * quirks. "fixed" runs the corrected estimator
- * (Q1-Q5, Q7, Q12, Q13 corrected). */
+ * (Q1-Q5, Q7, Q12, Q13 corrected, delta tracking included). */
 enum wost_compat { WOST_COMPAT_REFERENCE = 0, WOST_COMPAT_FIXED = 1 };
 
 /* ---------------------------------------------------------------------------
@@ -353,6 +353,15 @@ int wost_sampler_table(const wost_handle* h, float* out, int32_t n);
  * solvers/WoStSolver.py:250), evaluated on the host with the kernels' own
  * table and arithmetic: out[i] = G_norm(radii[i]). No device needed. */
 int wost_greens_norm(double sigma_bar, const float* radii, int64_t n, float* out);
+
+/* compat="fixed" delta tracking's radial sampler (quirks Q4/Q5 of
+ * ScreenedGreensDistribution2D, solvers/utils.py:154-195, corrected): the radius
+ * fraction rho[i] the walk kernels draw for uniform u[i] at the shape s[i] = R
+ * sqrt(sigma_bar), evaluated on the host with the kernels' table and arithmetic;
+ * and the exact CDF F_s(rho) of the ball's screened Green's radial law that it
+ * samples (closed form in I0, I1, K0, K1). No device needed. */
+int wost_screened_sample_fixed(const float* s, const float* u, int64_t n, float* rho);
+int wost_screened_cdf_fixed(double s, const double* rho, int64_t n, double* cdf);
 
 /* Batched polyline queries on the device (geometry/PolylinesSimple.py).
  *   op 0 distance          (:25-49, :214-224)   out_f[n]

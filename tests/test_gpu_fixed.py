@@ -1,5 +1,5 @@
 """compat="fixed": the Walk-on-Stars estimator with the reference's quirks
-corrected (Q1-Q3, Q7, Q12, Q13; wost_walk.h FIX).
+corrected (Q1-Q5, Q7, Q12, Q13; wost_walk.h FIX).
 
 The reference has no such mode, so there is nothing to be bit-identical to:
 these tests pin it by exact solutions instead. Each problem is chosen so that a
@@ -9,9 +9,11 @@ quirk the fixed mode corrects would bias the reference mode:
 * mixed Dirichlet / Neumann (u = x on the unit square, zero flux on top):
   Q1/Q2, the segment-parameter ray time and the rotated hemisphere, bias it;
 * Laplace (u = x^2 - y^2) and eps >= 1 (Q12).
-The fixed mode must agree with the exact solution within Monte-Carlo error,
-run bit-identically in the specialised and precompiled kernels, and refuse
-delta tracking (sigma/alpha), which it does not cover.
+* delta tracking (the reference's polynomial manufactured solution, and a mixed
+  problem with zero flux on one side): Q4/Q5, the clipped unit-ball screened law
+  without its Jacobian, biases compat="reference".
+The fixed mode must agree with the exact solution within Monte-Carlo error and
+run bit-identically in the specialised and precompiled kernels.
 """
 import numpy as np
 import pytest
@@ -114,8 +116,106 @@ def test_fixed_kernels_are_deterministic_and_agree(gpu_available, case):
     np.testing.assert_array_equal(v0, v2)
 
 
-def test_fixed_refuses_delta_tracking(gpu_available):
-    from dcrmontecarlo_amd.fields import X
+# ---------------------------------------------------------------- delta tracking (Q4/Q5)
+def _poly_problem():
+    """The reference's polynomial manufactured solution (tests/testWoStCorrectness.py:81-142):
+    u = (1-x^2)(1-y^2) on [-1,1]^2, diffusion alpha = 2 + x/2 + y/2, absorption
+    sigma = 2 + xy, f = -div(alpha grad u) + sigma u."""
+    from dcrmontecarlo_amd.fields import X, Y
 
-    with pytest.raises(NotImplementedError):
-        _solver(SQUARE1, X, f=1.0, sigma=1.0, compat="fixed")
+    u = (1 - X**2) * (1 - Y**2)
+    alpha = 2.0 + 0.5 * X + 0.5 * Y
+    sigma = 2.0 + X * Y
+    lap = -2.0 * (2.0 - X**2 - Y**2)
+    grad_dot = -X * (1 - Y**2) - Y * (1 - X**2)       # grad(alpha) . grad(u)
+    f = -(alpha * lap + grad_dot) + sigma * u
+    pts = np.array([[-0.5, 0.2], [0.0, 0.0], [0.6, -0.3], [0.3, 0.7], [-0.7, -0.6]], np.float32)
+    exact = (1 - pts[:, 0].astype(np.float64) ** 2) * (1 - pts[:, 1].astype(np.float64) ** 2)
+    return u, alpha, sigma, f, pts, exact
+
+
+def _mixed_problem():
+    """Unit square, Dirichlet on the left, bottom and right sides, zero-flux Neumann top:
+    u = 1 + x^2 + (1+x)(2y - y^2)/2 has u_y = 0 at y = 1; alpha = 1 + x/2, sigma = 1 + y.
+    The source is nonzero up to the Neumann side, so the walks' source samples on that
+    boundary (the half-ball) carry weight."""
+    from dcrmontecarlo_amd.fields import X, Y
+
+    u = 1.0 + X**2 + 0.5 * (1.0 + X) * (2.0 * Y - Y**2)
+    alpha = 1.0 + 0.5 * X
+    sigma = 1.0 + Y
+    lap = 1.0 - X                                        # u_xx + u_yy = 2 - (1 + x)
+    grad_dot = 0.5 * (2.0 * X + 0.5 * (2.0 * Y - Y**2))  # (1/2, 0) . grad(u)
+    f = -(alpha * lap + grad_dot) + sigma * u
+    pts = np.array([[0.3, 0.5], [0.5, 0.9], [0.7, 0.97], [0.2, 0.2], [0.5, 0.99]], np.float32)
+    x, y = pts[:, 0].astype(np.float64), pts[:, 1].astype(np.float64)
+    exact = 1 + x ** 2 + 0.5 * (1 + x) * (2 * y - y ** 2)
+    return u, alpha, sigma, f, pts, exact
+
+
+def test_fixed_delta_tracking_is_unbiased(gpu_available):
+    """Delta tracking with the corrected screened sampler (Q4/Q5) agrees with the exact
+    solution; the reference mode's clipped unit-ball law without the Jacobian does not."""
+    u, alpha, sigma, f, pts, exact = _poly_problem()
+    fixed = _solver(SQUARE1, u, f=f, sigma=sigma, alpha=alpha, compat="fixed")
+    assert fixed.use_delta_tracking and fixed.sigma_bar > 0
+    _, st = fixed.solve(pts, nWalks=400_000, maxSteps=2000, eps=1e-4, seed=21, return_stats=True)
+    assert np.all(np.abs(st.mean - exact) <= 5 * st.stderr + 2e-3), (st.mean, exact, st.stderr)
+    ref = _solver(SQUARE1, u, f=f, sigma=sigma, alpha=alpha)
+    _, sr = ref.solve(pts, nWalks=400_000, maxSteps=2000, eps=1e-4, seed=21, return_stats=True)
+    assert np.max(np.abs(_z(sr, exact))) > 10, "the reference-mode Q4/Q5 bias should be visible here"
+
+
+def test_fixed_delta_signed_collision_weights(gpu_available):
+    """sigma_bar below max sigma' (here 1.0 against ~2.9): the fixed mode keeps the
+    collision weight 1 - sigma'/sigma_bar signed and stays unbiased."""
+    u, alpha, sigma, f, pts, exact = _poly_problem()
+    s = _solver(SQUARE1, u, f=f, sigma=sigma, alpha=alpha, compat="fixed", sigma_bar=1.0)
+    assert s.sigma_bar == 1.0
+    _, st = s.solve(pts, nWalks=400_000, maxSteps=2000, eps=1e-4, seed=22, return_stats=True)
+    assert np.all(np.abs(st.mean - exact) <= 5 * st.stderr + 2e-3), (st.mean, exact, st.stderr)
+
+
+def test_fixed_mixed_delta_tracking_is_unbiased(gpu_available):
+    """Delta tracking with a Neumann side: nearest ray crossings (Q1), inward hemispheres
+    for the step and the source sample (Q2, Q13), collisions outside the star-shaped
+    region ending the walk, the corrected sampler (Q4/Q5)."""
+    u, alpha, sigma, f, pts, exact = _mixed_problem()
+    fixed = _solver(UNIT_U, u, UNIT_TOP, f=f, sigma=sigma, alpha=alpha, compat="fixed")
+    _, st = fixed.solve(pts, nWalks=400_000, maxSteps=4000, eps=1e-4, seed=23, return_stats=True)
+    assert np.all(np.abs(st.mean - exact) <= 5 * st.stderr + 2e-3), (st.mean, exact, st.stderr)
+
+
+def test_fixed_mixed_poisson_source_on_the_neumann_side(gpu_available):
+    """Poisson with a Neumann side and a source reaching it: on a Neumann boundary point the
+    source sample's direction is uniform on the inward hemisphere (the star-shaped region
+    is a half-ball). u = x^3 + 2y^3/3 - y^4/2 on the unit square: u_y = 2y^2 (1 - y) is 0 on
+    the top side, -lap u = -(6x + 4y - 6y^2)."""
+    from dcrmontecarlo_amd.fields import X, Y
+
+    g = X**3 + (2.0 / 3.0) * Y**3 - 0.5 * Y**4
+    f = -(6.0 * X + 4.0 * Y - 6.0 * Y**2)
+    pts = np.array([[0.3, 0.5], [0.5, 0.9], [0.7, 0.97], [0.5, 0.99]], np.float32)
+    x, y = pts[:, 0].astype(np.float64), pts[:, 1].astype(np.float64)
+    exact = x ** 3 + 2 * y ** 3 / 3 - y ** 4 / 2
+    s = _solver(UNIT_U, g, UNIT_TOP, f=f, compat="fixed")
+    _, st = s.solve(pts, nWalks=400_000, maxSteps=4000, eps=1e-4, seed=24, return_stats=True)
+    assert np.all(np.abs(st.mean - exact) <= 5 * st.stderr + 2e-3), (st.mean, exact, st.stderr)
+
+
+@pytest.mark.parametrize("case", ["delta", "mixed_delta"])
+def test_fixed_delta_kernels_are_deterministic_and_agree(gpu_available, case):
+    u, alpha, sigma, f, pts, _ = _poly_problem() if case == "delta" else _mixed_problem()
+    geo = (SQUARE1, None) if case == "delta" else (UNIT_U, UNIT_TOP)
+    mk = lambda: _solver(geo[0], u, geo[1], f=f, sigma=sigma, alpha=alpha, compat="fixed")
+    a = mk()
+    v0, s0 = a.solve_walks(pts, nWalks=8192, maxSteps=2000, eps=1e-4, seed=11)
+    v1, s1 = a.solve_walks(pts, nWalks=8192, maxSteps=2000, eps=1e-4, seed=11)
+    assert a.last_timing["jit"] == 1
+    np.testing.assert_array_equal(v0, v1)
+    b = mk()
+    b.set_jit(False)
+    v2, s2 = b.solve_walks(pts, nWalks=8192, maxSteps=2000, eps=1e-4, seed=11)
+    assert b.last_timing["jit"] == 0
+    np.testing.assert_array_equal(s0, s2)
+    np.testing.assert_array_equal(v0, v2)

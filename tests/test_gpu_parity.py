@@ -392,5 +392,5 @@ def test_edge_cases(gpu_available):
         s.solve(p, nWalks=0)
     with pytest.raises(ValueError):
         WostSolver_2D(sq, F.X, alpha=F.X + 2).solve(p, nWalks=4)   # delta tracking without a source (Q14)
-    with pytest.raises(NotImplementedError):   # compat="fixed" does not cover delta tracking
-        WostSolver_2D(sq, F.X, source=1.0, sigma=1.0, compat="fixed")
+    with pytest.raises(ValueError):             # unknown compat mode
+        WostSolver_2D(sq, F.X, source=1.0, sigma=1.0, compat="corrected")
