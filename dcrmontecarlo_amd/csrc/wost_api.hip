@@ -227,6 +227,11 @@ struct wost_handle {
 namespace {
 
 constexpr int64_t kMaxBatchWalks = int64_t(1) << 26;   // 64 Mi walks = 512 MiB of per-walk results
+// Above this many bytes of staged polylines per workgroup (4 workgroups of 256 on a
+// 160 KiB CU, 4 waves per SIMD) the field-specialised kernel reads the polylines from
+// global memory instead (wost_walk.h GL): long Dirichlet polylines, and long Neumann
+// polylines under compat="fixed" (which scans them), work at any length.
+constexpr size_t kGlobalPolylineLdsBytes = 40 * 1024;
 
 int upload_program(wost_handle* h) {
     if (!h->prog_dirty) return WOST_OK;
@@ -246,9 +251,11 @@ int upload_program(wost_handle* h) {
 // The field-specialised kernel for `mode` (with the walk recorder compiled in
 // when `record`), or nullptr when it is disabled or could not be built (the
 // precompiled kernel is used then; same results).
-hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock) {
+hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock,
+                         bool global_polylines = false) {
     if (!h->jit_enabled) return nullptr;
-    const int key = ((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 2 + (block != kWalkBlock ? 1 : 0);
+    const int key = (((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 2 + (block != kWalkBlock ? 1 : 0)) *
+                        2 + (global_polylines ? 1 : 0);
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
     h->jit_mode = key;
@@ -262,7 +269,7 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
     }
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
                                          (int)(h->dverts.size() / 2), h->nverts.data(), nn, record, ns, block,
-                                         phi.empty() ? nullptr : phi.data());
+                                         phi.empty() ? nullptr : phi.data(), global_polylines);
     std::string err;
     hipFunction_t fn = nullptr;
     if (!jit_get_kernel(h->device, src, &fn, &err)) {
@@ -786,7 +793,12 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
 
     int block = kWalkBlock;
     int tree_lds = h->jit_enabled ? tree_lds_records(h, mode, (int)std::min<int64_t>(n_points, INT32_MAX), &block) : 0;
-    hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block);
+    const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
+    // polylines whose LDS copy would cost the walk kernel its occupancy are read from
+    // global memory instead (field-specialised kernels; the precompiled ones stage them)
+    const bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds,
+                                                        jit_const_dirichlet(nd_)) > kGlobalPolylineLdsBytes;
+    hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly);
     if (!jfn && block != kWalkBlock) {   // the precompiled kernels run 256-thread workgroups, no staged tree
         block = kWalkBlock;
         tree_lds = 0;
@@ -794,9 +806,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if (ns > 1 && !jfn)
         return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
                     h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
-    const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
     const size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(nd_),
-                                      jfn && jit_const_neumann(mode, nn_));
+                                      jfn && jit_const_neumann(mode, nn_), jfn && gpoly);
     int blocks_per_cu = 0;
     if (jfn)
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));

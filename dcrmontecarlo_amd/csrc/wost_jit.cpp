@@ -32,11 +32,14 @@ namespace {
 // poly_distance_rcp). duu is formed exactly like the kernel forms it.
 // A/B switches for tools/ab_bench.sh (WOST_EXP_FLAGS, a bit mask; 0 in
 // production): 1 generic poly_distance for compiled-in polylines, 2 IEEE
-// unit_direction.
+// unit_direction. Ablations (timing studies only: the results are WRONG, the
+// walks merely stay statistically alike): 4 a cheap hash instead of Philox, 8 no
+// alpha(z) evaluation, 16 no sigma' at collisions, 32 no Neumann ray query;
+// 64 compiled-in silhouette scans unrolled by 4 only.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
-    return e ? (int)std::strtol(e, nullptr, 10) & 3 : 0;
+    return e ? (int)std::strtol(e, nullptr, 10) & 127 : 0;
 }
 
 // the squared segment length exactly as the kernel forms it
@@ -285,7 +288,7 @@ bool jit_const_neumann(int mode, int nn) {
 
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources,
-                         int block, const float* seg_phi) {
+                         int block, const float* seg_phi, bool global_polylines) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -296,6 +299,11 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     const DField& fA = hdr.field[SLOT_ALPHA];
     std::ostringstream o;
     if (exp_flags() & 2) o << "#define WOST_EXP_IEEE_DIRECTION 1\n";
+    if (exp_flags() & 4) o << "#define WOST_ABL_NO_PHILOX 1\n";
+    if (exp_flags() & 8) o << "#define WOST_ABL_NO_ALPHA_Z 1\n";
+    if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
+    if (exp_flags() & 32) o << "#define WOST_ABL_NO_RAY 1\n";
+    if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
@@ -363,11 +371,13 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         return v.str();
     };
     o << "    __device__ __forceinline__ float neumann_silhouette_distance(const float2* sN, int nn, float x, float y) const {\n";
-    if (nconst) o << nverts_decl() << "        return wost::silhouette_distance(v, " << nn << ", x, y);\n";
+    if (nconst) o << nverts_decl() << "        return wost::silhouette_distance<" << nn << ">(v, " << nn << ", x, y);\n";
     else o << "        return wost::silhouette_distance(sN, nn, x, y);\n";
     o << "    }\n";
     o << "    __device__ __forceinline__ wost::Hit neumann_intersect(const float2* sN, int nn, float x, float y, float dx,"
          " float dy, float r) const {\n";
+    // (a two-pass variant -- filter pass, then one exact division per lane -- measured
+    // slower on C3's 32-segment circle: 1.24e10 vs 1.94e10 walk-steps/s, r02 ab_perf3)
     if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
     else o << "        return wost::intersect_polylines<false>(sN, nn, x, y, dx, dy, r);\n";
     o << "    }\n";
@@ -389,7 +399,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
       << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
       << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
-      << ", " << n_sources << ", " << (mode_fix(mode) ? "true" : "false") << ">(A, fld, smem);\n}\n";
+      << ", " << n_sources << ", " << (mode_fix(mode) ? "true" : "false") << ", "
+      << (global_polylines ? "true" : "false") << ">(A, fld, smem);\n}\n";
     return o.str();
 }
 

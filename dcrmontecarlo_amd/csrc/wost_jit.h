@@ -34,10 +34,13 @@ bool jit_const_neumann(int mode, int nn);
 // sources SLOT_F, SLOT_EXTRA.. (multi-source batching).
 // `block`: threads per workgroup the kernel is launched with; seg_phi: the
 // device's per-segment normal angles of a compiled-in Neumann polyline (nn - 1
-// floats, read back from the setup kernel so the constants carry its bits).
+// floats, read back from the setup kernel so the constants carry its bits);
+// global_polylines: the kernel reads polylines that are not compiled in from
+// global memory instead of staging them in LDS (wost_walk.h GL).
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record,
-                         int n_sources = 1, int block = 256, const float* seg_phi = nullptr);
+                         int n_sources = 1, int block = 256, const float* seg_phi = nullptr,
+                         bool global_polylines = false);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

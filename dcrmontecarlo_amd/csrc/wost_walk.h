@@ -81,7 +81,9 @@ WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 //  * with the segment tree, its first tree_lds records (64 B each).
 // Query points are read from global memory (once per walk, at refill).
 WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false,
-                                  bool delta = false, int tree_lds = 0, bool const_d = false, bool const_n = false) {
+                                  bool delta = false, int tree_lds = 0, bool const_d = false, bool const_n = false,
+                                  bool global_polylines = false) {
+    if (global_polylines) const_d = const_n = true;   // nothing of the polylines is staged
     (void)n_points;
     size_t b = 0;
     if (src) b += delta ? sizeof(float4) * (size_t)kGnormCells : 16;
@@ -137,15 +139,21 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 //  boundary, and its weight 1 - sigma'/sigma_bar is kept signed (unbiased for
 //  any sigma_bar; the reference's max(., 0) at solvers/WoStSolver.py:282 is
 //  biased wherever sigma' > sigma_bar).
-template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, bool FIX = false, class F>
+// GL: the polylines (and segment angles) are read from global memory instead of being
+// staged in LDS -- field-specialised kernels for polylines too long for the LDS budget
+// (wost_api.hip kGlobalPolylineLdsBytes).
+template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, bool FIX = false, bool GL = false,
+          class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
     // the walk's position updates round op by op like the reference (torch CPU
     // has no FMA contraction); the field math it calls keeps its own setting
 #pragma clang fp contract(off)
     static_assert(NS >= 1 && (NS == 1 || SRC) && (NS == 1 || !REC), "multi-source walks need a source, no recorder");
     static_assert(!(FIX && TREE), "compat=fixed runs the scan queries");
-    constexpr bool kStageD = !F::kConstDirichlet;
-    constexpr bool kStageN = NEU && !TREE && (!F::kConstNeumann || FIX);   // FIX scans sN itself
+    constexpr bool kStageD = !F::kConstDirichlet && !GL;
+    // the Neumann polyline is staged also when compiled in (FIX scans sN itself; a few
+    // hundred bytes otherwise)
+    constexpr bool kStageN = NEU && !TREE && !GL;
     unsigned char* lds = smem;
     float4* sG = reinterpret_cast<float4*>(lds);                          // G_norm cells
     float* sT = reinterpret_cast<float*>(lds + (DELTA ? sizeof(float4) * (size_t)kGnormCells : 16));  // sampler tail
@@ -166,6 +174,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     }
     if (TREE)   // the top levels of the segment tree (wost_device.h SegTree, child records)
         for (int i = threadIdx.x; i < 4 * A.tree_lds_records; i += blockDim.x) sTree[i] = A.tree[i];
+    // the polylines the queries read: the LDS copies, or (GL) global memory
+    const float2* const dP = GL ? A.dverts : sD;
+    const float2* const nP = GL ? A.nverts : sN;
+    const float* const phiP = GL ? A.seg_phi : sPhi;
     const SegTree tree{A.tree, TREE ? sTree : nullptr, TREE ? A.tree_lds_records : 0, A.nverts, A.nn,
                        A.tree_first_leaf, A.tree_leaf, A.tree_tol};
     float node0 = 0.0f;
@@ -194,6 +206,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     // per-lane walk state (solvers/WoStSolver.py:188-195)
     bool active = false;
     uint64_t wid = 0;           // global walk id: the Philox subsequence
+    PhiloxWalk pw{0u, 0u, 0u, 0u};   // its per-walk Philox words (philox_walk)
     uint64_t lid = 0;           // local walk index: the output slot
     float px = 0.f, py = 0.f;
     float dD = 1.0f;            // dDirichlet seeded with 1.0 (:190, quirk Q12)
@@ -262,6 +275,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                     if (rem < 0) --pid;
                     else if (rem >= A.walks_per_point) ++pid;
                 }
+                pw = philox_walk(wid, A.key0, A.key1);
                 const float2 q = A.points[pid];
                 px = q.x; py = q.y;
                 k = 0; dD = FIX ? WOST_INF : 1.0f; onB = false; phi = 0.f; w = 1.f;
@@ -279,7 +293,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         if (!(active && (k < A.max_steps) && (dD > A.eps))) continue;
 
         // --- one walk-step (:206-291)
-        const float dd = fld.dirichlet_distance(sD, A.nd, px, py);  // :208
+        const float dd = fld.dirichlet_distance(dP, A.nd, px, py);  // :208
         if (FIX && !(dd > A.eps)) {   // Q7/Q12 fixed: stop here, g at this point
             dD = dd;
             continue;
@@ -288,7 +302,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
         if (NEU) {
             const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
-                                  : fld.neumann_silhouette_distance(sN, A.nn, px, py);  // :211
+                                  : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
             dnv = dn;
             const float m = dn < dd ? dn : dd;                       // Python min()
             r = m > A.rmin ? m : A.rmin;                             // Python max() (:212)
@@ -296,8 +310,12 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             r = dd > A.rmin ? dd : A.rmin;                           // :215
         }
 
-        const U4 rn = philox4x32_10(U4{(uint32_t)k, 0u, (uint32_t)wid, (uint32_t)(wid >> 32)},
-                                    A.key0, A.key1);
+#if defined(WOST_ABL_NO_PHILOX)   // ablation (timing only): a cheap hash
+        const uint32_t hh = (pw.b ^ (uint32_t)k * 0x9E3779B9u) * 0x85EBCA6Bu;
+        const U4 rn{hh, hh * 0xC2B2AE35u, (hh ^ pw.d) * 0x27D4EB2Fu, hh ^ pw.c};
+#else
+        const U4 rn = philox_draw(pw, (uint32_t)k, A.key0, A.key1);   // philox4x32_10({k, 0, wid})
+#endif
         float theta = (u01(rn.x) * 2.0f) * kPiF;                     // :226
         // :227-228 (quirk Q2): atan2(normal) is a property of the segment that
         // was hit, precomputed per segment with the same device atan2f
@@ -308,15 +326,19 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 
         float xnx, xny;
         if (NEU) {                                                   // :235-236
-            const Hit h = FIX ? intersect_polylines_ray(sN, A.nn, px, py, cs, sn, r)
+#if defined(WOST_ABL_NO_RAY)
+            Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
+#else
+            const Hit h = FIX ? intersect_polylines_ray(nP, A.nn, px, py, cs, sn, r)
                               : TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
-                                     : fld.neumann_intersect(sN, A.nn, px, py, cs, sn, r);
+                                     : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
+#endif
             xnx = h.x; xny = h.y; onB = h.hit;
-            if (h.hit) phi = TREE ? A.seg_phi[h.seg] : fld.neumann_phi(sPhi, h.seg);
+            if (h.hit) phi = TREE ? A.seg_phi[h.seg] : fld.neumann_phi(phiP, h.seg);
             if (FIX && h.hit) {
                 // inward normal: the left normal when the ray crossed the segment from
                 // its left side, i.e. cross(d, u) > 0 (then dot(left normal, d) < 0)
-                const float2 a = sN[h.seg], b = sN[h.seg + 1];
+                const float2 a = nP[h.seg], b = nP[h.seg + 1];
                 if (!(cs * (b.y - a.y) - sn * (b.x - a.x) > 0.0f)) phi = phi + kPiF;
             }
         } else {                                                     // :238-239
@@ -341,7 +363,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 const float cs2 = f_cos(ts), sn2 = f_sin(ts);
                 yx = px + rs * cs2;
                 yy = py + rs * sn2;
-                if (NEU) clipped = intersect_polylines_ray(sN, A.nn, px, py, cs2, sn2, rs).hit;   // not visible
+                if (NEU) clipped = intersect_polylines_ray(nP, A.nn, px, py, cs2, sn2, rs).hit;   // not visible
             } else {
                 // :245 (quirk Q13). FIX delta keeps the sample on the step's ray: with the
                 // nearest crossing (Q1) the clip below is exactly "y is in the star-shaped
@@ -422,9 +444,15 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             // the two branches share the weight update w * sqrt(a_new / alpha(x));
             // only the field evaluations stay divergent
             float anew = aj.v;                                       // collision, or a clipped accept
+#if !defined(WOST_ABL_NO_ALPHA_Z)
             if (accept && !clipped) anew = fld.alpha(xnx, xny);      // :277
+#endif
             float sc = 1.0f;
+#if defined(WOST_ABL_NO_SIGMA_PRIME)
+            if (false) {
+#else
             if (!accept) {
+#endif
                 const float spv = sigma_prime_from(aj, fld.sigma(yx, yy), fld.detached());  // :281
                 sc = 1.0f - spv * inv_sb;
                 sc = (0.0f > sc) ? 0.0f : sc;                        // Python max(., 0.0) (:282)

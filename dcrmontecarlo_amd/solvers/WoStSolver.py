@@ -204,17 +204,21 @@ class WostSolver_2D:
             self._h = None
 
     # ---- setters (solvers/WoStSolver.py:141-157) ------------------------------
+    # the attribute changes only once libwost has accepted the field, so that it always
+    # describes what the device solves
     def setBoundaryConditions(self, boundaryDirichlet):
-        self.boundaryDirichlet = self._conv(boundaryDirichlet, "boundaryDirichlet")
-        wf, keep = _lib.make_field(self.boundaryDirichlet)
+        g = self._conv(boundaryDirichlet, "boundaryDirichlet")
+        wf, keep = _lib.make_field(g)
         _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_BOUNDARY, ctypes.pointer(wf) if wf else None),
                    "setBoundaryConditions")
+        self.boundaryDirichlet = g
 
     def setSourceTerm(self, source):
-        self.source = self._conv(source, "source")
-        wf, keep = _lib.make_field(self.source)
+        f = self._conv(source, "source")
+        wf, keep = _lib.make_field(f)
         _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_SOURCE, ctypes.pointer(wf) if wf else None),
                    "setSourceTerm")
+        self.source = f
 
     # ---- sigma' as a callable, like the reference's attribute ----------------
     def sigma_prime(self, point):
@@ -312,6 +316,14 @@ class WostSolver_2D:
             raise ValueError("nWalks must be >= 1")
         sums = np.zeros((n, 3), np.float64)
         if return_history:
+            # the recorder keeps maxSteps + 1 records per walk on the host: refuse sizes the
+            # host cannot hold before allocating (WOST_HISTORY_MAX_BYTES, default 8 GiB)
+            rec_bytes = n * nWalks * (int(maxSteps) + 1) * _lib.REC_FLOATS * 4
+            limit = int(os.environ.get("WOST_HISTORY_MAX_BYTES", str(8 << 30)))
+            if rec_bytes > limit:
+                raise ValueError(f"return_history needs {rec_bytes / 2**30:.1f} GiB of walk records "
+                                 f"({n} points x {nWalks} walks x {int(maxSteps) + 1} records); lower maxSteps, "
+                                 f"nWalks or the point count, or raise WOST_HISTORY_MAX_BYTES ({limit} bytes)")
             wv = np.empty(n * nWalks, np.float32)
             ws = np.empty(n * nWalks, np.uint32)
             stride = int(maxSteps) + 1
