@@ -54,8 +54,8 @@ def test_invalid_problems_are_rejected_before_device_use():
 
     with pytest.raises(ValueError, match=">= 2 vertices"):
         WostSolver_2D(PolyLinesSimple(np.zeros((1, 2), np.float32)), F.X)
-    with pytest.raises(NotImplementedError):
-        WostSolver_2D(PolyLinesSimple(np.zeros((3, 2), np.float32)), F.X, source=1.0, sigma=1.0, compat="fixed")
+    with pytest.raises(ValueError, match="non-finite"):
+        WostSolver_2D(PolyLinesSimple(np.array([[0, 0], [1, np.nan], [1, 1]], np.float32)), F.X, compat="fixed")
     with pytest.raises(ValueError, match="compat"):
         WostSolver_2D(PolyLinesSimple(np.zeros((3, 2), np.float32)), F.X, compat="corrected")
     with pytest.raises(TypeError, match="a field, a number or a callable"):
