@@ -281,7 +281,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 k = 0; dD = FIX ? WOST_INF : 1.0f; onB = false; phi = 0.f; w = 1.f;
 #pragma unroll
                 for (int s = 0; s < NS; ++s) total[s] = 0.f;
+#if defined(WOST_ABL_NO_POINT_ALPHA)
+                if (DELTA) ax = 100.0f;
+#else
                 if (DELTA) ax = fld.alpha(px, py);
+#endif
                 active = true;
             }
             c_next += take;
