@@ -191,6 +191,7 @@ struct wost_handle {
     // field-specialised walk kernel (wost_jit.cpp)
     bool jit_enabled = true;
     hipFunction_t jit_fn = nullptr;
+    hipFunction_t jit_alpha_fn = nullptr;   // the same module's wost_point_alpha_jit (delta modes)
     int jit_mode = -1;
     uint64_t jit_version = ~0ull;
     std::string jit_error;
@@ -221,6 +222,8 @@ struct wost_handle {
     int64_t bstats_cap = 0;
     float2* d_points = nullptr;
     int64_t points_cap = 0;
+    float* d_point_alpha = nullptr;   // alpha at the query points (delta tracking)
+    int64_t point_alpha_cap = 0;
     wost_timing timing{};
 };
 
@@ -258,6 +261,7 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
                         2 + (global_polylines ? 1 : 0);
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
+    h->jit_alpha_fn = nullptr;
     h->jit_mode = key;
     h->jit_version = h->prog_version;
     const int nn = (int)(h->nverts.size() / 2);
@@ -272,13 +276,19 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
                                          phi.empty() ? nullptr : phi.data(), global_polylines);
     std::string err;
     hipFunction_t fn = nullptr;
-    if (!jit_get_kernel(h->device, src, &fn, &err)) {
+    hipFunction_t afn = nullptr;
+    if (!jit_get_kernel(h->device, src, &fn, &err, &afn)) {
         h->jit_error = err;
         std::fprintf(stderr, "libwost: field-specialised kernel unavailable, using the precompiled one: %s\n",
                      err.c_str());
         return nullptr;
     }
+    if (mode_delta(mode) && !afn) {
+        h->jit_error = "the specialised module has no wost_point_alpha_jit";
+        return nullptr;
+    }
     h->jit_fn = fn;
+    h->jit_alpha_fn = afn;
     return fn;
 }
 
@@ -497,7 +507,7 @@ void wost_destroy(wost_handle* h) {
     if (!h) return;
     if (h->device >= 0) (void)hipSetDevice(h->device);
     void* ptrs[] = {h->d_dverts, h->d_nverts, h->d_table, h->d_prog, h->d_counter, h->d_val,
-                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree, h->d_seg_phi};
+                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree, h->d_seg_phi, h->d_point_alpha};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t& e : h->ev)
@@ -845,6 +855,22 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_tol = h->tree.tol;
         a.tree_stop2 = silhouette_stop2(a.rmin);
         a.tree_lds_records = tree_lds;
+    }
+
+    if (mode_delta(mode) && n_points > 0) {   // alpha at the query points, with the walk kernel's fields
+        if ((rc = ensure_cap(h->d_point_alpha, h->point_alpha_cap, n_points)) != WOST_OK) return rc;
+        if (jfn) {
+            const float2* pts = h->d_points;
+            long long n = (long long)n_points;
+            float* out = h->d_point_alpha;
+            const char* prog = h->d_prog;
+            void* args[] = {&prog, &pts, &n, &out};
+            const int grid = (int)std::min<int64_t>((n_points + 255) / 256, 4096);
+            HIP_TRY(hipModuleLaunchKernel(h->jit_alpha_fn, grid, 1, 1, 256, 1, 1, 0, h->stream, args, nullptr));
+        } else {
+            HIP_TRY(launch_point_alpha(h->d_prog, h->d_points, n_points, h->d_point_alpha, h->stream));
+        }
+        a.point_alpha = h->d_point_alpha;
     }
 
     std::vector<int64_t> begins;

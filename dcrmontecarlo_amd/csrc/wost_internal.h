@@ -64,6 +64,9 @@ inline size_t table_floats(bool delta, bool fixed_delta = false) {
 }
 
 
+// alpha at the query points with the interpreted fields (delta tracking)
+hipError_t launch_point_alpha(const char* prog, const float2* pts, int64_t n, float* out, hipStream_t s);
+
 // precompiled (interpreted-field) walk kernels
 hipError_t walk_occupancy(int mode, int nd, int nn, int n_points, int* blocks_per_cu);
 hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s);

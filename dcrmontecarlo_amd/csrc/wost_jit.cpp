@@ -35,12 +35,11 @@ namespace {
 // unit_direction. Ablations (timing studies only: the results are WRONG, the
 // walks merely stay statistically alike): 4 a cheap hash instead of Philox, 8 no
 // alpha(z) evaluation, 16 no sigma' at collisions, 32 no Neumann ray query;
-// 64 compiled-in silhouette scans unrolled by 4 only, 128 no alpha at the start
-// point of a walk (refill).
+// 64 compiled-in silhouette scans unrolled by 4 only.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
-    return e ? (int)std::strtol(e, nullptr, 10) & 255 : 0;
+    return e ? (int)std::strtol(e, nullptr, 10) & 127 : 0;
 }
 
 // the squared segment length exactly as the kernel forms it
@@ -224,6 +223,7 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
 struct Entry {
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
+    hipFunction_t alpha_fn = nullptr;   // wost_point_alpha_jit, when the source has it
 };
 
 std::mutex g_mu;
@@ -305,7 +305,6 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
     if (exp_flags() & 32) o << "#define WOST_ABL_NO_RAY 1\n";
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
-    if (exp_flags() & 128) o << "#define WOST_ABL_NO_POINT_ALPHA 1\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
@@ -403,10 +402,17 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
       << ", " << n_sources << ", " << (mode_fix(mode) ? "true" : "false") << ", "
       << (global_polylines ? "true" : "false") << ">(A, fld, smem);\n}\n";
+    if (delta)   // alpha at the query points, with these fields (WalkArgs::point_alpha)
+        o << "extern \"C\" __global__ void __launch_bounds__(256)\n"
+          << "wost_point_alpha_jit(const char* prog, const float2* pts, long long n, float* out) {\n"
+          << "    const GenFields fld{reinterpret_cast<const float*>(prog + "
+          << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
+          << "    wost::point_alpha_body(pts, (int64_t)n, out, fld);\n}\n";
     return o.str();
 }
 
-bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err) {
+bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err,
+                    hipFunction_t* alpha_fn) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
         *err = "hipGetDeviceProperties failed";
@@ -427,6 +433,7 @@ bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, st
     auto it = g_modules.find(key);
     if (it != g_modules.end()) {
         *fn = it->second.fn;
+        if (alpha_fn) *alpha_fn = it->second.alpha_fn;
         return true;
     }
     std::vector<char> code;
@@ -449,8 +456,11 @@ bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, st
         *err = "hipModuleGetFunction(wost_walk_jit) failed";
         return false;
     }
+    if (hipModuleGetFunction(&e.alpha_fn, e.mod, "wost_point_alpha_jit") != hipSuccess) e.alpha_fn = nullptr;
+    (void)hipGetLastError();   // a source without the alpha kernel leaves a lookup error behind
     g_modules[key] = e;
     *fn = e.fn;
+    if (alpha_fn) *alpha_fn = e.alpha_fn;
     return true;
 }
 

@@ -44,6 +44,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.
-bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err);
+// alpha_fn (optional): the source's wost_point_alpha_jit kernel (delta tracking), or null.
+bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err,
+                    hipFunction_t* alpha_fn = nullptr);
 
 }  // namespace wost

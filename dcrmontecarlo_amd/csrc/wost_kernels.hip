@@ -133,6 +133,20 @@ wost_walk_kernel(const WalkArgs A) {
     walk_body<NEU, SRC, DELTA, TREE, true, 1, FIX>(A, fld, smem);   // records when A.rec is set
 }
 
+// alpha at the query points (WalkArgs::point_alpha) with the interpreted fields
+__global__ void __launch_bounds__(256) wost_point_alpha_kernel(const char* prog, const float2* pts, int64_t n,
+                                                               float* out) {
+    const InterpFields fld(prog);
+    point_alpha_body(pts, n, out, fld);
+}
+
+hipError_t launch_point_alpha(const char* prog, const float2* pts, int64_t n, float* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+    wost_point_alpha_kernel<<<grid, 256, 0, s>>>(prog, pts, n, out);
+    return hipGetLastError();
+}
+
 // mode -> kernel instantiation (MODE_* of wost_internal.h)
 #define WOST_FOR_MODE(mode, X)                                   \
     switch (mode) {                                              \

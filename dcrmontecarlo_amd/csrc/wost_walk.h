@@ -57,7 +57,21 @@ struct WalkArgs {
     int64_t range_offset;
     int64_t range_point0;
     double inv_range_walks;
+    // delta tracking: alpha at each query point (point_alpha_body, same fields and
+    // arithmetic as the walk's own alpha), read at a walk's start instead of
+    // evaluating the field there
+    const float* point_alpha;
 };
+
+// alpha at the query points with the walk kernel's own Fields policy (the same
+// function the walk would evaluate at its start point, hence the same bits).
+template <class F>
+__device__ __forceinline__ void point_alpha_body(const float2* pts, int64_t n, float* out, const F& fld) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float2 q = pts[i];
+        out[i] = fld.alpha(q.x, q.y);
+    }
+}
 
 constexpr int kWalkBlock = 256;
 
@@ -281,11 +295,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 k = 0; dD = FIX ? WOST_INF : 1.0f; onB = false; phi = 0.f; w = 1.f;
 #pragma unroll
                 for (int s = 0; s < NS; ++s) total[s] = 0.f;
-#if defined(WOST_ABL_NO_POINT_ALPHA)
-                if (DELTA) ax = 100.0f;
-#else
-                if (DELTA) ax = fld.alpha(px, py);
-#endif
+                if (DELTA) ax = A.point_alpha[pid];                // alpha(x0), precomputed per point
                 active = true;
             }
             c_next += take;
