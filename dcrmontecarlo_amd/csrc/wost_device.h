@@ -136,8 +136,13 @@ WOST_HD float f_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 WOST_HD float f_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
 WOST_HD float f_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 WOST_HD float f_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
+#if defined(WOST_EXP_LIBM_SINCOS)   // A/B: the device library's accurate sinf/cosf
+WOST_HD float f_sin(float x) { return sinf(x); }
+WOST_HD float f_cos(float x) { return cosf(x); }
+#else
 WOST_HD float f_sin(float x) { return __sinf(x); }
 WOST_HD float f_cos(float x) { return __cosf(x); }
+#endif
 WOST_HD float f_log(float x) { return __logf(x); }
 #else
 WOST_HD float f_exp(float x) { return expf(x); }

@@ -35,11 +35,12 @@ namespace {
 // unit_direction. Ablations (timing studies only: the results are WRONG, the
 // walks merely stay statistically alike): 4 a cheap hash instead of Philox, 8 no
 // alpha(z) evaluation, 16 no sigma' at collisions, 32 no Neumann ray query;
-// 64 compiled-in silhouette scans unrolled by 4 only.
+// 64 compiled-in silhouette scans unrolled by 4 only, 128 the device library's
+// accurate sinf/cosf for the step direction instead of v_sin/v_cos.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
-    return e ? (int)std::strtol(e, nullptr, 10) & 127 : 0;
+    return e ? (int)std::strtol(e, nullptr, 10) & 255 : 0;
 }
 
 // the squared segment length exactly as the kernel forms it
@@ -305,6 +306,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
     if (exp_flags() & 32) o << "#define WOST_ABL_NO_RAY 1\n";
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
+    if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
