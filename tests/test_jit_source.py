@@ -18,12 +18,14 @@ HIPRTC_OPTS = ["-O3", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt", 
 def test_generated_sources_name_their_variant():
     src = S.dcr_dipole().kernel_source()
     assert "walk kernel, mode 5" in src and "wost_walk_jit" in src
-    assert "walk_body<true, true, true, false, false, 1, false>" in src
+    assert "walk_body<true, true, true, false, false, 1, false, false>" in src
+    assert "wost_point_alpha_jit" in src                    # alpha at the query points (delta)
     assert "const float2 v[5]" in src                       # the square compiled in
     topo = S.wenner_topography(n_electrodes=4, n_walks=1).kernel_source()
-    assert "walk_body<true, true, true, true, false, 1, false>" in topo      # the 10k-segment surface uses the tree
+    assert "walk_body<true, true, true, true, false, 1, false, false>" in topo      # the 10k-segment surface uses the tree
     lap = S.laplace_square().kernel_source()
-    assert "walk_body<false, false, false, false, false, 1, false>" in lap
+    assert "walk_body<false, false, false, false, false, 1, false, false>" in lap
+    assert "wost_point_alpha_jit" not in lap
 
 
 def _tabulated_source():
@@ -48,7 +50,7 @@ def test_tabulated_fields_are_generated():
     assert "reinterpret_cast<const float*>(A.prog + " in src
 
 
-def _fixed_source():
+def _fixed_source(delta=False):
     import numpy as np
 
     from dcrmontecarlo_amd.fields import X, Y
@@ -57,12 +59,14 @@ def _fixed_source():
 
     D = PolyLinesSimple(np.array([[0, 1], [0, 0], [1, 0], [1, 1]], np.float32))
     N = PolyLinesSimple(np.array([[1, 1], [0, 1]], np.float32))
+    if delta:   # compat="fixed" delta tracking (the corrected screened sampler)
+        return kernel_source(D, X, N, source=1.0 + X * Y, sigma=1.0 + Y, alpha=1.0 + 0.5 * X, compat="fixed")
     return kernel_source(D, X, N, source=1.0 + X * Y, compat="fixed")
 
 
 def test_generated_sources_compile_for_gfx950():
     names = ["laplace_square", "poisson_square", "variable_coefficients", "dcr_dipole", "wenner_topography",
-             "tabulated", "fixed_mixed_poisson"]
+             "tabulated", "fixed_mixed_poisson", "fixed_mixed_delta"]
     with tempfile.TemporaryDirectory() as d:
         procs = []
         for n in names:
@@ -70,7 +74,10 @@ def test_generated_sources_compile_for_gfx950():
                 src = _tabulated_source()
             elif n == "fixed_mixed_poisson":   # compat="fixed" (wost_walk.h FIX)
                 src = _fixed_source()
-                assert "walk_body<true, true, false, false, false, 1, true>" in src
+                assert "walk_body<true, true, false, false, false, 1, true, false>" in src
+            elif n == "fixed_mixed_delta":
+                src = _fixed_source(delta=True)
+                assert "walk_body<true, true, true, false, false, 1, true, false>" in src
             else:
                 sc = S.ALL[n]() if n != "wenner_topography" else S.wenner_topography(n_electrodes=4, n_walks=1)
                 src = sc.kernel_source()
