@@ -923,12 +923,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
         const int64_t waves = (int64_t)grid * (block / 64);
         a.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(1024, count / (waves * 4)));
-        // the last ~4 walks per lane go out 64 at a time (one per lane of a wave): a
-        // 1024-walk chunk is ~16 walks per lane, and the wave that takes one as the queue
-        // runs dry would otherwise run alone for that long
-        a.tail_chunk = std::min<int>(a.chunk, 64);
-        a.n_big = std::max<int64_t>(0, count - waves * 64 * 4) / a.chunk;
-        a.tail_begin = a.n_big * a.chunk;
+        // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
+        // on C4 and 10-14% slower on the short-walk scenarios: profiles/r02_ab/guided_queue.log)
         h->timing.grid_blocks = grid;
 
         HIP_TRY(hipEventRecord(h->ev[0], h->stream));

@@ -6,9 +6,6 @@
 //
 // One walk per lane:
 //  * persistent waves; each lane holds one walk's state in registers;
-//  * a guided work queue: one atomic hands a wave the next chunk of walk ids --
-//    large chunks first, small ones for the last few walks per lane, so that the
-//    waves run out of work together;
 //  * when walks finish, the wave re-fills those lanes by __ballot / __popcll
 //    rank from a chunk of walk ids it dequeued with one atomic (active-mask
 //    compaction, so short walks never idle a lane for long);
@@ -39,7 +36,7 @@ struct WalkArgs {
     float eps;
     float rmin;                  // eps / 2 (solvers/WoStSolver.py:167)
     uint32_t key0, key1;         // Philox key = seed
-    int32_t chunk;               // walks claimed per work-queue dequeue (before tail_begin)
+    int32_t chunk;               // walks claimed per work-queue dequeue
     int32_t n_points;            // query points
     double inv_walks_per_point;  // 1/W for the point index of a walk id
     const float* seg_phi;        // [nn-1] atan2 of each Neumann segment's left normal
@@ -64,12 +61,6 @@ struct WalkArgs {
     // arithmetic as the walk's own alpha), read at a walk's start instead of
     // evaluating the field there
     const float* point_alpha;
-    // guided work queue: dequeue j claims walks [j chunk, (j+1) chunk) below tail_begin
-    // (= n_big chunk), then tail_chunk walks each, so that the waves finish together
-    int64_t tail_begin;
-    int64_t n_big;
-    int32_t tail_chunk;
-    int32_t pad2_;
 };
 
 // alpha at the query points with the walk kernel's own Fields policy (the same
@@ -265,22 +256,14 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         while (need != 0ull && !exhausted) {
             if (c_next >= c_end) {
                 unsigned long long c = 0;
-                if (lane == 0) c = atomicAdd(A.counter, 1ull);   // the dequeue's index
+                if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)A.chunk);
                 c = __shfl(c, 0);
-                uint64_t b, len;
-                if (c < (uint64_t)A.n_big) {
-                    b = c * (uint64_t)A.chunk;
-                    len = (uint64_t)A.chunk;
-                } else {
-                    b = (uint64_t)A.tail_begin + (c - (uint64_t)A.n_big) * (uint64_t)A.tail_chunk;
-                    len = (uint64_t)A.tail_chunk;
-                }
-                if (b >= (uint64_t)A.count) {
+                if (c >= (unsigned long long)A.count) {
                     exhausted = true;
                     break;
                 }
-                c_next = b;
-                c_end = b + len;
+                c_next = c;
+                c_end = c + (uint64_t)A.chunk;
                 if (c_end > (uint64_t)A.count) c_end = (uint64_t)A.count;
             }
             const uint64_t avail = c_end - c_next;
