@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--only", default="")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--compat", default="reference", help="reference | fixed (non-delta scenarios only)")
+    ap.add_argument("--compat", default="reference", help="reference | fixed")
     ap.add_argument("--scan", action="store_true", help="force the full Neumann scans (no segment tree)")
     a = ap.parse_args()
     names = a.only.split(",") if a.only else list(SIZES)
@@ -34,8 +34,6 @@ def main():
         npts, W = SIZES[name]
         W = max(1, int(W * a.scale))
         sc = S.ALL[name]()
-        if a.compat != "reference" and (sc.sigma is not None or sc.alpha is not None):
-            continue
         solver = sc.solver(device=int(os.environ.get("LOCAL_RANK", "0")), compat=a.compat)
         if a.scan:
             solver.set_segment_tree(-1)
