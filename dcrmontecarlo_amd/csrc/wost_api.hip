@@ -816,8 +816,10 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if (ns > 1 && !jfn)
         return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
                     h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
-    const size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(nd_),
-                                      jfn && jit_const_neumann(mode, nn_), jfn && gpoly);
+    size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(nd_),
+                                jfn && jit_const_neumann(mode, nn_), jfn && gpoly);
+    // A/B knob (occupancy studies): WOST_LDS_PAD_BYTES extra bytes of LDS per workgroup
+    if (const char* e = std::getenv("WOST_LDS_PAD_BYTES")) lds += (size_t)std::max(0, std::atoi(e));
     int blocks_per_cu = 0;
     if (jfn)
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
@@ -906,6 +908,10 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
             if (j2 == j) return fail(WOST_ERR_INVALID_ARG, "internal: block larger than a batch");
             count = blk_end(j2 - 1) - wb;
             a.wid_begin = wb;
+            a.base_pid = wb / W;
+            const int64_t off = wb - a.base_pid * W;
+            a.base_off = (uint32_t)std::min<int64_t>(off, INT32_MAX);
+            a.small32 = (W < (int64_t(1) << 31) && off + count < (int64_t(1) << 31)) ? 1 : 0;
             a.range_walks = 0;
         }
         begins.push_back(count);

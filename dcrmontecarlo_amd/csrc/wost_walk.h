@@ -61,6 +61,12 @@ struct WalkArgs {
     // arithmetic as the walk's own alpha), read at a walk's start instead of
     // evaluating the field there
     const float* point_alpha;
+    // 32-bit point index of a walk (the refill's quotient): wid_begin = base_pid * W +
+    // base_off, and when base_off + count < 2^31 (small32) the quotient of base_off +
+    // local index by W is taken in 32 bits (a double estimate and one correction)
+    int64_t base_pid;
+    uint32_t base_off;
+    int32_t small32;
 };
 
 // alpha at the query points with the walk kernel's own Fields policy (the same
@@ -276,12 +282,22 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 // (exact operands below 2^53) and one correction
                 uint64_t pid;
                 if (A.range_walks > 0) {
-                    uint64_t q = (uint64_t)((double)lid * A.inv_range_walks);
-                    int64_t rem = (int64_t)(lid - q * (uint64_t)A.range_walks);
-                    if (rem < 0) { --q; rem += A.range_walks; }
-                    else if (rem >= A.range_walks) { ++q; rem -= A.range_walks; }
+                    // local index < 2^26 (one launch): a 32-bit quotient
+                    const uint32_t l32 = (uint32_t)lid, rw = (uint32_t)A.range_walks;
+                    uint32_t q = (uint32_t)((double)l32 * A.inv_range_walks);
+                    int32_t rem = (int32_t)(l32 - q * rw);
+                    if (rem < 0) { --q; rem += (int32_t)rw; }
+                    else if (rem >= (int32_t)rw) { ++q; rem -= (int32_t)rw; }
                     pid = (uint64_t)A.range_point0 + q;
                     wid = pid * (uint64_t)A.walks_per_point + (uint64_t)A.range_offset + (uint64_t)rem;
+                } else if (A.small32) {
+                    const uint32_t local = A.base_off + (uint32_t)lid, w32 = (uint32_t)A.walks_per_point;
+                    uint32_t q = (uint32_t)((double)local * A.inv_walks_per_point);
+                    const int32_t rem = (int32_t)(local - q * w32);
+                    if (rem < 0) --q;
+                    else if (rem >= (int32_t)w32) ++q;
+                    pid = (uint64_t)A.base_pid + q;
+                    wid = (uint64_t)A.wid_begin + lid;
                 } else {
                     wid = (uint64_t)A.wid_begin + lid;
                     pid = (uint64_t)((double)wid * A.inv_walks_per_point);
