@@ -315,7 +315,10 @@ def main():
                                        "(wost_solve_distributed: libwost RCCL all-gather of block sums)")
                        if world > 1 else "one GPU"},
             "roofline": {"bound": "valu", "achieved": ach_tflops, "peak": perfmodel.FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": ach_tflops / perfmodel.FP32_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": ach_tflops / perfmodel.FP32_PEAK_TFLOPS,
+                         # HBM bytes per walk-kernel launch from the committed PMC passes
+                         # (profiles/traffic_dcr_dipole.json) vs the algorithmic 8 B per walk
+                         "traffic": measured_traffic(), "algorithmic_bytes_per_launch": bytes_per_launch,
                          "model_flops_per_step": fps, "flop_model": "SURVEY.md 8(d) v1 per-config total (C4 ~350)",
                          "kernel": "wost_walk_jit (hiprtc field-specialised, mixed+delta)" if jit
                          else "wost_walk_kernel<true,true,true> (precompiled)",
