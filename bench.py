@@ -233,7 +233,9 @@ def main():
     # libwost's own RCCL communicator (wost_comm_*): the 128-byte id travels through the
     # launcher's TCP store; barriers, the block-sum all-gather and the max over ranks
     # are RCCL collectives on libwost's stream -- no torch process group
-    comm = C.Communicator.from_env(device=local) if world > 1 else None
+    # (WOST_BENCH_FORCE_COMM=1 takes the communicator path with one rank too: a check of the
+    # launcher bootstrap and the RCCL solve on a one-GPU box)
+    comm = C.Communicator.from_env(device=local) if (world > 1 or os.environ.get("WOST_BENCH_FORCE_COMM")) else None
     # weak: N x 1M walks per electrode over N GPUs; strong: 1M walks per electrode over N
     Wt = sc.n_walks * (world if args.scaling == "weak" else 1)   # walks per electrode of the whole job
     w0, w1 = C.shard_walk_range(Wt, world, rank)

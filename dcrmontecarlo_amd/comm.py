@@ -89,7 +89,7 @@ class Communicator:
         rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
-        if world == 1:
+        if world == 1 and "MASTER_PORT" not in os.environ:   # a lone process: no store needed
             return cls(unique_id(), 1, 0, device)
         uid, store = exchange_over_store(unique_id, key, timeout)
         c = cls(uid, world, rank, device)
