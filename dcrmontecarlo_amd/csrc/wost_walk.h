@@ -263,7 +263,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             if (c_next >= c_end) {
                 unsigned long long c = 0;
                 if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)A.chunk);
-                c = __shfl(c, 0);
+                // lane 0's value as a scalar (every lane runs the refill): the queue
+                // state stays in SGPRs and the refill loop's control flow uniform
+                c = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(c >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c);
                 if (c >= (unsigned long long)A.count) {
                     exhausted = true;
                     break;
