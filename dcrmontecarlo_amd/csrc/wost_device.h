@@ -368,6 +368,38 @@ WOST_HD Jet fj_sigmoid_radial(float x, float y, float k, float cx, float cy, flo
     // z = k (d - R): grad z = k (x-c)/d, lap z = k/d (2-D), |grad z|^2 = k^2
     return Jet{s, s1 * k * dx * inv, s1 * k * dy * inv, s2 * k * k + s1 * k * inv};
 }
+// ---- whole-field saturation (the specialised kernels' alpha jets) ------------
+// When every factor of a field is saturated at a point -- sharp sigmoids exactly
+// 0 or 1, Gaussians exactly 0, indicators -- every factor jet's derivatives are
+// signed zeros (s1 = s2 = 0, e = 0), and so are the field jet's, except that a
+// radial factor exactly at its centre (d2 = 0: inv = +inf times a zero) makes
+// them NaN. Their only consumer, sigma_prime_from, squares the gradient and adds
+// the Laplacian to 1e-8, so the signs of those zeros never reach sigma': the
+// jet {value, z, z, z} (z = 0, or NaN at a centre) gives its bits without the
+// derivative arithmetic. Each predicate keeps a margin to the thresholds its
+// factor's own shortcut uses (radial_saturation; z >= 20 / <= -90; q < -110), so
+// a saturated lane is one whose full jet is saturated whatever the rounding.
+WOST_HD bool sat_sigmoid_radial(float x, float y, float k, float cx, float cy, float R, bool& centre) {
+    const float dx = x - cx, dy = y - cy;
+    const float d2 = dx * dx + dy * dy;
+    const RadialSat sat = radial_saturation(k, R);
+    centre = centre || !(d2 > 0.0f);
+    return d2 >= sat.hi2 || d2 <= sat.lo2;
+}
+WOST_HD bool sat_sigmoid_lin(float x, float y, float a, float b, float c) {
+    const float z = a * x + b * y + c;
+    return z >= 21.0f || z <= -91.0f;
+}
+WOST_HD bool sat_exp_quad_diag(float x, float y, float cx, float cy, float axx, float ayy) {
+    const float dx = x - cx, dy = y - cy;
+    return axx * (dx * dx) + ayy * (dy * dy) < kExpZeroBelow - 1.0f;
+}
+WOST_HD bool sat_exp_quad(float x, float y, float cx, float cy, float axx, float ayy, float axy, float ax, float ay,
+                          float a0) {
+    const float dx = x - cx, dy = y - cy;
+    return axx * (dx * dx) + ayy * (dy * dy) + axy * (dx * dy) + ax * dx + ay * dy + a0 < kExpZeroBelow - 1.0f;
+}
+
 WOST_HD Jet fj_ind_box(float x, float y, float x0, float x1, float y0, float y1) {
     return jet_const(fv_ind_box(x, y, x0, x1, y0, y1));
 }

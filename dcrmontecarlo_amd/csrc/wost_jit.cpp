@@ -36,11 +36,12 @@ namespace {
 // walks merely stay statistically alike): 4 a cheap hash instead of Philox, 8 no
 // alpha(z) evaluation, 16 no sigma' at collisions, 32 no Neumann ray query;
 // 64 compiled-in silhouette scans unrolled by 4 only, 128 the device library's
-// accurate sinf/cosf for the step direction instead of v_sin/v_cos.
+// accurate sinf/cosf for the step direction instead of v_sin/v_cos; 512 no
+// whole-field saturation shortcut in the alpha jet (jet_body).
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
-    return e ? (int)std::strtol(e, nullptr, 10) & 255 : 0;
+    return e ? (int)std::strtol(e, nullptr, 10) & 0xFFFF : 0;
 }
 
 // the squared segment length exactly as the kernel forms it
@@ -160,9 +161,67 @@ std::string value_body(const DField& fd, const DTerm* terms, const DFactor* fact
     return o.str();
 }
 
-// Same operation sequence as wost::field_jet.
-std::string jet_body(const DField& fd, const DTerm* terms, const DFactor* factors) {
+// The saturation predicate of a factor (wost_device.h sat_*), "true" for the
+// indicators (zero derivatives everywhere), "" for a kind without one.
+std::string sat_call(const DFactor& f) {
+    const float* p = f.p;
     std::ostringstream o;
+    switch (f.kind) {
+    case WOST_FK_SIGMOID_RADIAL:
+        o << "wost::sat_sigmoid_radial(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ", "
+          << lit(p[3]) << ", centre)";
+        break;
+    case WOST_FK_SIGMOID_LIN:
+        o << "wost::sat_sigmoid_lin(x, y, " << lit(p[0]) << ", " << lit(p[1]) << ", " << lit(p[2]) << ")";
+        break;
+    case WOST_FK_EXP_QUAD: {
+        const bool diag = exp_quad_is_diag(p);
+        o << (diag ? "wost::sat_exp_quad_diag(x, y" : "wost::sat_exp_quad(x, y");
+        for (int k = 0; k < (diag ? 4 : 8); ++k) o << ", " << lit(p[k]);
+        o << ")";
+        break;
+    }
+    case WOST_FK_IND_BOX:
+    case WOST_FK_IND_DISK:
+        return "true";
+    default:
+        return "";
+    }
+    return o.str();
+}
+
+// Same operation sequence as wost::field_jet. When every factor has a saturation
+// predicate and the coefficients are finite, a wave whose lanes are all saturated
+// returns {value, z, z, z} (wost_device.h, whole-field saturation): the value from
+// `value_fn` (the field's value body, the same bits as the jet's value there).
+std::string jet_body(const DField& fd, const DTerm* terms, const DFactor* factors, const char* value_fn = nullptr) {
+    std::ostringstream o;
+    if (value_fn != nullptr && !(exp_flags() & 512)) {
+        std::ostringstream s;
+        bool ok = fd.n_terms > 0, radial = false;
+        for (int t = 0; t < fd.n_terms && ok; ++t) {
+            const DTerm& tm = terms[fd.first_term + t];
+            ok = std::isfinite(tm.coef);
+            for (int k = 0; k < tm.nf && ok; ++k) {
+                const DFactor& f = factors[tm.first + k];
+                const std::string c = sat_call(f);
+                ok = !c.empty();
+                radial |= f.kind == WOST_FK_SIGMOID_RADIAL;
+                if (ok && c != "true") s << (s.tellp() > 0 ? " & " : "") << c;
+            }
+        }
+        if (ok && s.tellp() > 0) {
+            o << "        {\n"
+              << "            bool centre = false;\n"
+              << "            const bool sat = " << s.str() << ";\n"
+              << "            if (WOST_SAT_ALL(sat)) {\n"
+              << "                const float z = " << (radial ? "centre ? __builtin_nanf(\"\") : 0.0f" : "0.0f")
+              << ";\n"
+              << "                return wost::Jet{" << value_fn << "(x, y), z, z, z};\n"
+              << "            }\n"
+              << "        }\n";
+        }
+    }
     o << "        wost::Jet acc = wost::jet_const(0.0f);\n";
     for (int t = 0; t < fd.n_terms; ++t) {
         const DTerm& tm = terms[fd.first_term + t];
@@ -329,7 +388,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    __device__ __forceinline__ float alpha(float x, float y) const {\n"
       << (fA.present ? value_body(fA, terms, factors) : "        return 1.0f;\n") << "    }\n";
     o << "    __device__ __forceinline__ wost::Jet alpha_jet(float x, float y) const {\n"
-      << (fA.present ? jet_body(fA, terms, factors) : "        return wost::jet_const(1.0f);\n") << "    }\n";
+      << (fA.present ? jet_body(fA, terms, factors, (fA.flags & WOST_FIELD_DETACHED) ? nullptr : "alpha") : "        return wost::jet_const(1.0f);\n") << "    }\n";
     o << "    __device__ __forceinline__ bool detached() const { return "
       << ((fA.flags & WOST_FIELD_DETACHED) ? "true" : "false") << "; }\n";
     o << "    __device__ __forceinline__ float sigma_bar() const { return " << lit(hdr.sigma_bar) << "; }\n";

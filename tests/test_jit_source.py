@@ -21,6 +21,13 @@ def test_generated_sources_name_their_variant():
     assert "walk_body<true, true, true, false, false, 1, false, false>" in src
     assert "wost_point_alpha_jit" in src                    # alpha at the query points (delta)
     assert "const float2 v[5]" in src                       # the square compiled in
+    # whole-field saturation shortcut of the alpha jet (two smooth circles + a constant)
+    assert src.count("wost::sat_sigmoid_radial(x, y, ") == 2 and "if (WOST_SAT_ALL(sat))" in src
+    assert "return wost::Jet{alpha(x, y), z, z, z};" in src
+    nb = S.notebook_dcr().kernel_source()                   # + sigmoid(10000 y): linear sigmoid predicate
+    assert "wost::sat_sigmoid_lin(x, y, " in nb and nb.count("wost::sat_sigmoid_radial(x, y, ") == 2
+    vc = S.variable_coefficients().kernel_source()          # detached alpha (Q9): no jet shortcut needed
+    assert "if (WOST_SAT_ALL(sat))" not in vc
     topo = S.wenner_topography(n_electrodes=4, n_walks=1).kernel_source()
     assert "walk_body<true, true, true, true, false, 1, false, false>" in topo      # the 10k-segment surface uses the tree
     lap = S.laplace_square().kernel_source()
