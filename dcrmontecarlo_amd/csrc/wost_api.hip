@@ -412,11 +412,13 @@ bool use_tree(const wost_handle* h) {
 int walk_mode(const wost_handle* h) {
     const bool neu = !h->nverts.empty();
     const bool src = h->fields[SLOT_F].present;
-    if (h->compat == WOST_COMPAT_FIXED) {   // scan queries (no segment tree)
-        if (h->delta) return neu ? MODE_FIX_MIXED_DELTA : MODE_FIX_DELTA;
-        return neu ? (src ? MODE_FIX_MIXED_POISSON : MODE_FIX_MIXED) : (src ? MODE_FIX_POISSON : MODE_FIX_DIRICHLET);
-    }
     const bool tree = neu && use_tree(h);
+    if (h->compat == WOST_COMPAT_FIXED) {   // the nearest-crossing ray queries (scan or tree)
+        if (h->delta) return neu ? (tree ? MODE_FIX_MIXED_DELTA_TREE : MODE_FIX_MIXED_DELTA) : MODE_FIX_DELTA;
+        if (neu) return src ? (tree ? MODE_FIX_MIXED_POISSON_TREE : MODE_FIX_MIXED_POISSON)
+                            : (tree ? MODE_FIX_MIXED_TREE : MODE_FIX_MIXED);
+        return src ? MODE_FIX_POISSON : MODE_FIX_DIRICHLET;
+    }
     if (h->delta) return neu ? (tree ? MODE_MIXED_DELTA_TREE : MODE_MIXED_DELTA) : MODE_DELTA;
     if (neu) return src ? (tree ? MODE_MIXED_POISSON_TREE : MODE_MIXED_POISSON) : (tree ? MODE_MIXED_TREE : MODE_MIXED);
     return src ? MODE_POISSON : MODE_DIRICHLET;

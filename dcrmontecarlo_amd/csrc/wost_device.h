@@ -31,7 +31,11 @@
 // guarded expression (an exp, a square root) for every lane and select the result,
 // which costs the transcendental issue slots the guard is there to save.
 #define WOST_NO_SPECULATION() __asm__ volatile("" ::: "memory")
+// A wave-uniform value the compiler must treat as redefined here (kept in an SGPR):
+// what is computed from it after this point is not hoisted out of the loop.
+#define WOST_OPAQUE_SGPR(v) __asm__ volatile("" : "+s"(v))
 #else
+#define WOST_OPAQUE_SGPR(v) ((void)0)
 #define WOST_ANY(c) (c)
 #define WOST_NO_SPECULATION() ((void)0)
 #endif
@@ -924,6 +928,42 @@ WOST_HD float2 segment_left_normal(float2 sa, float2 sb) {
     return float2{-ey, ex};
 }
 
+// The ray parameter t of the crossing of segment a->b by the ray q + t d that the
+// reference's test accepts (s in [0, 1], t > 0; :104-132), when t < best, else
+// +inf; both divisions only for candidates of the hardware-reciprocal filter.
+WOST_HD float ray_segment_nearest_t(float2 a, float2 b, float qx, float qy, float dx, float dy, float best) {
+#pragma clang fp contract(off)
+    const float ux = b.x - a.x, uy = b.y - a.y;
+    const float wx = qx - a.x, wy = qy - a.y;
+    const float den = dx * uy - dy * ux;
+    const float rd = f_rcp(den);
+    const float ns = dx * wy - dy * wx, nt = ux * wy - uy * wx;
+    const float sa = ns * rd, ta = nt * rd;
+    float res = WOST_INF;
+    if (sa >= -1e-6f && sa <= 1.000001f && ta > -1e-6f && ta < best * 1.000001f + 1e-30f) {
+        const float s = ns / den, t = nt / den;
+        if (s >= 0.0f && s <= 1.0f && t > 0.0f && t < best) res = t;
+    }
+    return res;
+}
+
+// The nearest-crossing query's hit (bi, best) or miss (intersect_polylines_ray).
+WOST_HD Hit ray_nearest_finish(int bi, float best, float px, float py, float dx, float dy, float qx, float qy,
+                               float r) {
+#pragma clang fp contract(off)
+    Hit h;
+    if (bi < 0 || best > r) {
+        h.x = px + r * dx; h.y = py + r * dy; h.nx = 0.f; h.ny = 0.f; h.hit = false; h.seg = -1;
+        return h;
+    }
+    h.x = qx + best * dx;
+    h.y = qy + best * dy;
+    h.nx = 0.f; h.ny = 0.f;
+    h.hit = true;
+    h.seg = bi;
+    return h;
+}
+
 // compat="fixed" ray query (quirk Q1 corrected): the nearest crossing along
 // the ray, i.e. the least RAY parameter t over the segments the reference's
 // test accepts (s in [0, 1], t > 0), a hit when t <= r at q + t d. The
@@ -944,28 +984,11 @@ WOST_HD Hit intersect_polylines_ray(VP v, int nv, float px, float py, float dxi,
     float2 a = v[0];
     for (int i = 1; i < nv; ++i) {
         const float2 b = v[i];
-        const float ux = b.x - a.x, uy = b.y - a.y;
-        const float wx = qx - a.x, wy = qy - a.y;
-        const float den = dx * uy - dy * ux;
-        const float rd = f_rcp(den);
-        const float ns = dx * wy - dy * wx, nt = ux * wy - uy * wx;
-        const float sa = ns * rd, ta = nt * rd;
-        if (sa >= -1e-6f && sa <= 1.000001f && ta > -1e-6f && ta < best * 1.000001f + 1e-30f) {
-            const float s = ns / den, t = nt / den;
-            if (s >= 0.0f && s <= 1.0f && t > 0.0f && t < best) { best = t; bi = i - 1; }
-        }
+        const float t = ray_segment_nearest_t(a, b, qx, qy, dx, dy, best);
+        if (t < best) { best = t; bi = i - 1; }
         a = b;
     }
-    if (bi < 0 || best > r) {
-        h.x = px + r * dx; h.y = py + r * dy; h.nx = 0.f; h.ny = 0.f; h.hit = false; h.seg = -1;
-        return h;
-    }
-    h.x = qx + best * dx;
-    h.y = qy + best * dy;
-    h.nx = 0.f; h.ny = 0.f;
-    h.hit = true;
-    h.seg = bi;
-    return h;
+    return ray_nearest_finish(bi, best, px, py, dx, dy, qx, qy, r);
 }
 
 // :179-197 -- the hit (or miss) from the winning segment bi and its "time".
@@ -1211,7 +1234,11 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
 }
 
 // intersect_polylines over the tree: the same winner as the full scan.
-template <bool NORMAL = true>
+// NEAREST (compat="fixed"): intersect_polylines_ray's nearest crossing instead --
+// the same line pruning (every segment that test accepts lies on the ray's line
+// within tol as well), the same per-segment test, and leaves in ascending segment
+// order, so the strict t < best keeps the scan's first argmin; the same bits.
+template <bool NORMAL = true, bool NEAREST = false>
 WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
     Hit h;
@@ -1265,13 +1292,19 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
             float2 a = t.v[s0];
             for (int i = s0; i < s1; ++i) {
                 const float2 b = t.v[i + 1];
-                const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
-                if (s < best) { best = s; bi = i; }
+                if (NEAREST) {
+                    const float tt = ray_segment_nearest_t(a, b, qx, qy, dx, dy, best);
+                    if (tt < best) { best = tt; bi = i; }
+                } else {
+                    const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
+                    if (s < best) { best = s; bi = i; }
+                }
                 a = b;
             }
         }
         live = resume();
     }
+    if (NEAREST) return ray_nearest_finish(bi, best, px, py, dx, dy, qx, qy, r);
     return intersect_finish<NORMAL>(t.v, bi, best, px, py, dx, dy, qx, qy, r);
 }
 

@@ -21,18 +21,26 @@ enum WalkMode : int {
     MODE_MIXED_TREE = 6,
     MODE_MIXED_POISSON_TREE = 7,
     MODE_MIXED_DELTA_TREE = 8,
-    // compat="fixed" estimators (wost_walk.h FIX): Laplace, Poisson, mixed (scan queries)
+    // compat="fixed" estimators (wost_walk.h FIX): Laplace, Poisson, mixed (Neumann scans)
     MODE_FIX_DIRICHLET = 9,
     MODE_FIX_POISSON = 10,
     MODE_FIX_MIXED = 11,
     MODE_FIX_MIXED_POISSON = 12,
     // compat="fixed" delta tracking (Q4/Q5 corrected sampler), Dirichlet only / + Neumann
     MODE_FIX_DELTA = 13,
-    MODE_FIX_MIXED_DELTA = 14
+    MODE_FIX_MIXED_DELTA = 14,
+    // compat="fixed" mixed modes with the Neumann queries through the segment tree
+    MODE_FIX_MIXED_TREE = 15,
+    MODE_FIX_MIXED_POISSON_TREE = 16,
+    MODE_FIX_MIXED_DELTA_TREE = 17,
+    MODE_COUNT = 18
 };
 
-inline bool mode_fix(int m) { return m >= MODE_FIX_DIRICHLET && m <= MODE_FIX_MIXED_DELTA; }
-inline bool mode_tree(int m) { return m >= MODE_MIXED_TREE && m <= MODE_MIXED_DELTA_TREE; }
+inline bool mode_fix(int m) { return m >= MODE_FIX_DIRICHLET && m <= MODE_FIX_MIXED_DELTA_TREE; }
+inline bool mode_tree(int m) {
+    return (m >= MODE_MIXED_TREE && m <= MODE_MIXED_DELTA_TREE) ||
+           (m >= MODE_FIX_MIXED_TREE && m <= MODE_FIX_MIXED_DELTA_TREE);
+}
 inline bool mode_neu(int m) {
     return m == MODE_MIXED || m == MODE_MIXED_POISSON || m == MODE_MIXED_DELTA || mode_tree(m) ||
            m == MODE_FIX_MIXED || m == MODE_FIX_MIXED_POISSON || m == MODE_FIX_MIXED_DELTA;
@@ -40,11 +48,12 @@ inline bool mode_neu(int m) {
 inline bool mode_src(int m) {
     return m == MODE_POISSON || m == MODE_MIXED_POISSON || m == MODE_DELTA || m == MODE_MIXED_DELTA ||
            m == MODE_MIXED_POISSON_TREE || m == MODE_MIXED_DELTA_TREE || m == MODE_FIX_POISSON ||
-           m == MODE_FIX_MIXED_POISSON || m == MODE_FIX_DELTA || m == MODE_FIX_MIXED_DELTA;
+           m == MODE_FIX_MIXED_POISSON || m == MODE_FIX_DELTA || m == MODE_FIX_MIXED_DELTA ||
+           m == MODE_FIX_MIXED_POISSON_TREE || m == MODE_FIX_MIXED_DELTA_TREE;
 }
 inline bool mode_delta(int m) {
     return m == MODE_DELTA || m == MODE_MIXED_DELTA || m == MODE_MIXED_DELTA_TREE || m == MODE_FIX_DELTA ||
-           m == MODE_FIX_MIXED_DELTA;
+           m == MODE_FIX_MIXED_DELTA || m == MODE_FIX_MIXED_DELTA_TREE;
 }
 
 // const_d: the kernel has the Dirichlet polyline compiled in (field-specialised

@@ -165,6 +165,9 @@ hipError_t launch_point_alpha(const char* prog, const float2* pts, int64_t n, fl
     case MODE_FIX_MIXED_POISSON: X(true, true, false, false, true);   \
     case MODE_FIX_DELTA: X(false, true, true, false, true);           \
     case MODE_FIX_MIXED_DELTA: X(true, true, true, false, true);      \
+    case MODE_FIX_MIXED_TREE: X(true, false, false, true, true);      \
+    case MODE_FIX_MIXED_POISSON_TREE: X(true, true, false, true, true); \
+    case MODE_FIX_MIXED_DELTA_TREE: X(true, true, true, true, true);  \
     default: return hipErrorInvalidValue;                        \
     }
 

@@ -169,7 +169,6 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     // has no FMA contraction); the field math it calls keeps its own setting
 #pragma clang fp contract(off)
     static_assert(NS >= 1 && (NS == 1 || SRC) && (NS == 1 || !REC), "multi-source walks need a source, no recorder");
-    static_assert(!(FIX && TREE), "compat=fixed runs the scan queries");
     constexpr bool kStageD = !F::kConstDirichlet && !GL;
     // the Neumann polyline is staged also when compiled in (FIX scans sN itself; a few
     // hundred bytes otherwise)
@@ -347,7 +346,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         const uint32_t hh = (pw.b ^ (uint32_t)k * 0x9E3779B9u) * 0x85EBCA6Bu;
         const U4 rn{hh, hh * 0xC2B2AE35u, (hh ^ pw.d) * 0x27D4EB2Fu, hh ^ pw.c};
 #else
-        const U4 rn = philox_draw(pw, (uint32_t)k, A.key0, A.key1);   // philox4x32_10({k, 0, wid})
+        // the key enters each step opaque, so its round schedule (key + r * W) is
+        // formed by scalar adds here instead of 16 loop-invariant SGPRs, which the
+        // register allocator would otherwise spill to VGPR lanes (a v_readlane each)
+        uint32_t key0 = A.key0, key1 = A.key1;
+        WOST_OPAQUE_SGPR(key0);
+        WOST_OPAQUE_SGPR(key1);
+        const U4 rn = philox_draw(pw, (uint32_t)k, key0, key1);       // philox4x32_10({k, 0, wid})
 #endif
         float theta = (u01(rn.x) * 2.0f) * kPiF;                     // :226
         // :227-228 (quirk Q2): atan2(normal) is a property of the segment that
@@ -362,7 +367,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #if defined(WOST_ABL_NO_RAY)
             Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
 #else
-            const Hit h = FIX ? intersect_polylines_ray(nP, A.nn, px, py, cs, sn, r)
+            const Hit h = FIX ? (TREE ? intersect_polylines_tree<false, true>(tree, px, py, cs, sn, r)
+                                      : intersect_polylines_ray(nP, A.nn, px, py, cs, sn, r))
                               : TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
                                      : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
 #endif
@@ -371,7 +377,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             if (FIX && h.hit) {
                 // inward normal: the left normal when the ray crossed the segment from
                 // its left side, i.e. cross(d, u) > 0 (then dot(left normal, d) < 0)
-                const float2 a = nP[h.seg], b = nP[h.seg + 1];
+                const float2* const sv = TREE ? A.nverts : nP;   // the tree kernels stage none
+                const float2 a = sv[h.seg], b = sv[h.seg + 1];
                 if (!(cs * (b.y - a.y) - sn * (b.x - a.x) > 0.0f)) phi = phi + kPiF;
             }
         } else {                                                     // :238-239
@@ -396,7 +403,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 const float cs2 = f_cos(ts), sn2 = f_sin(ts);
                 yx = px + rs * cs2;
                 yy = py + rs * sn2;
-                if (NEU) clipped = intersect_polylines_ray(nP, A.nn, px, py, cs2, sn2, rs).hit;   // not visible
+                if (NEU)   // not visible
+                    clipped = TREE ? intersect_polylines_tree<false, true>(tree, px, py, cs2, sn2, rs).hit
+                                   : intersect_polylines_ray(nP, A.nn, px, py, cs2, sn2, rs).hit;
             } else {
                 // :245 (quirk Q13). FIX delta keeps the sample on the step's ray: with the
                 // nearest crossing (Q1) the clip below is exactly "y is in the star-shaped

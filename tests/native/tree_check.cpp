@@ -95,4 +95,25 @@ int tree_check_stop(const float* xy, int nv, int leaf, const float* pts, const f
     return 0;
 }
 
+// compat="fixed": the nearest-crossing ray query over the tree
+// (intersect_polylines_tree<false, true>) against intersect_polylines_ray's scan,
+// bit for bit (x, y, hit, segment). out[0] = mismatches, out[1] = hits.
+int tree_check_nearest(const float* xy, int nv, int leaf, const float* pts, const float* dirs, const float* radii,
+                       long n, long* out) {
+    SegmentTreeHost th;
+    if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
+    const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), nullptr, 0, reinterpret_cast<const float2*>(xy),
+                    nv, th.first_leaf, th.leaf, th.tol};
+    const float2* v = reinterpret_cast<const float2*>(xy);
+    out[0] = out[1] = 0;
+    for (long i = 0; i < n; ++i) {
+        const float px = pts[2 * i], py = pts[2 * i + 1];
+        const Hit hb = intersect_polylines_ray(v, nv, px, py, dirs[2 * i], dirs[2 * i + 1], radii[i]);
+        const Hit ht = intersect_polylines_tree<false, true>(t, px, py, dirs[2 * i], dirs[2 * i + 1], radii[i]);
+        if (!same(hb.x, ht.x) || !same(hb.y, ht.y) || hb.hit != ht.hit || hb.seg != ht.seg) ++out[0];
+        if (hb.hit) ++out[1];
+    }
+    return 0;
+}
+
 }  // extern "C"

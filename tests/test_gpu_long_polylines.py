@@ -42,11 +42,14 @@ def test_long_dirichlet_polyline_global_reads(gpu_available):
 
 
 def test_long_neumann_polyline_under_fixed_compat(gpu_available):
-    """compat="fixed" scans the Neumann polyline (no segment tree): a 6000-segment
-    zero-flux line y = 0 across the rectangle [0,1] x [-0.5,1] (Dirichlet all round),
-    u = x harmonic with u_y = 0 on it. A ray through a vertex of the line can slip
-    between its two segments in float arithmetic; such a walk then ends on the lower
-    Dirichlet side, where u = x holds as well, so the exact solution stands."""
+    """compat="fixed" on a 6000-segment zero-flux line y = 0 across the rectangle
+    [0,1] x [-0.5,1] (Dirichlet all round), u = x harmonic with u_y = 0 on it. The
+    nearest-crossing queries through the segment tree (field-specialised and
+    precompiled kernels) give the bits of the full scans (the specialised kernel
+    reading the line from global memory, the precompiled one staging it). A ray
+    through a vertex of the line can slip between its two segments in float
+    arithmetic; such a walk then ends on the lower Dirichlet side, where u = x holds
+    as well, so the exact solution stands."""
     from dcrmontecarlo_amd.fields import X
     from dcrmontecarlo_amd.geometry import PolyLinesSimple
     from dcrmontecarlo_amd.solvers import WostSolver_2D
@@ -62,6 +65,13 @@ def test_long_neumann_polyline_under_fixed_compat(gpu_available):
     v1, s1 = b.solve_walks(pts, nWalks=1024, maxSteps=2000, eps=1e-3, seed=7)
     np.testing.assert_array_equal(s0, s1)
     np.testing.assert_array_equal(v0, v1)
+    for jit in (True, False):                                      # the scans
+        c = WostSolver_2D(PolyLinesSimple(D), X, PolyLinesSimple(N), compat="fixed")
+        c.set_jit(jit)
+        c.set_segment_tree(-1)
+        v2, s2 = c.solve_walks(pts, nWalks=1024, maxSteps=2000, eps=1e-3, seed=7)
+        np.testing.assert_array_equal(s0, s2)
+        np.testing.assert_array_equal(v0, v2)
     _, st = a.solve(pts, nWalks=50_000, maxSteps=2000, eps=1e-3, seed=8, return_stats=True)
     assert np.all(np.abs(st.mean - pts[:, 0]) <= 5 * st.stderr + 3e-3), (st.mean, pts[:, 0])
 
@@ -75,3 +85,19 @@ def test_history_size_is_checked_before_allocating(gpu_available, monkeypatch):
     monkeypatch.setenv("WOST_HISTORY_MAX_BYTES", str(1 << 20))
     with pytest.raises(ValueError, match="return_history"):
         s.solve(np.full((100, 2), 0.5, np.float32), nWalks=1000, maxSteps=1000, return_history=True)
+
+
+def test_fixed_topography_tree_equals_scan(gpu_available):
+    """C5's 10k-segment topography under compat="fixed" (delta tracking, mixed):
+    the tree kernel's walks are bitwise those of the full scan."""
+    from dcrmontecarlo_amd import scenarios as S
+
+    sc = S.wenner_topography(n_electrodes=16, n_walks=1, n_segments=10_000)
+    a = sc.solver(device=0, compat="fixed")
+    b = sc.solver(device=0, compat="fixed")
+    b.set_segment_tree(-1)
+    pts = sc.points[::4]
+    v0, s0 = a.solve_walks(pts, nWalks=256, maxSteps=200, eps=sc.eps, seed=3)
+    v1, s1 = b.solve_walks(pts, nWalks=256, maxSteps=200, eps=sc.eps, seed=3)
+    np.testing.assert_array_equal(s0, s1)
+    np.testing.assert_array_equal(v0, v1)

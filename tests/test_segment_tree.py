@@ -33,6 +33,9 @@ def harness(tmp_path_factory):
     lib.tree_check.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, fp, fp, ctypes.c_long,
                                ctypes.POINTER(ctypes.c_long)]
     lib.tree_check.restype = ctypes.c_int
+    lib.tree_check_nearest.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, fp, ctypes.c_long,
+                                       ctypes.POINTER(ctypes.c_long)]
+    lib.tree_check_nearest.restype = ctypes.c_int
     lib.tree_check_stop.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_float,
                                     ctypes.c_long, ctypes.POINTER(ctypes.c_long)]
     lib.tree_check_stop.restype = ctypes.c_int
@@ -170,3 +173,36 @@ def test_gpu_tree_walks_match_scan_walks(gpu_available):
     for key, (v, st) in res.items():
         np.testing.assert_array_equal(st, ref[1], err_msg=str(key))
         np.testing.assert_array_equal(v.view(np.uint32), ref[0].view(np.uint32), err_msg=str(key))
+
+
+def run_nearest(lib, verts, pts, dirs, radii, leaf=8):
+    f = lambda a: np.ascontiguousarray(a, np.float32)
+    verts, pts, dirs, radii = f(verts), f(pts), f(dirs), f(radii)
+    out = (ctypes.c_long * 2)()
+    p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    assert lib.tree_check_nearest(p(verts), verts.shape[0], leaf, p(pts), p(dirs), p(radii), pts.shape[0], out) == 0
+    return list(out)
+
+
+@pytest.mark.parametrize("leaf", [1, 8, 32])
+def test_tree_nearest_crossing_matches_scan(harness, leaf):
+    """compat="fixed" (Q1 corrected): the nearest crossing along the ray through the
+    tree equals intersect_polylines_ray's full scan bit for bit -- the hit point and
+    the segment whose normal the walk turns on -- on the 10k-segment topography and
+    a closed zig-zag (ties at shared vertices keep the lower segment index)."""
+    rng = np.random.default_rng(77 + leaf)
+    topo = S.topography(10_000)
+    pts, dirs, radii, _ = queries(rng, topo.astype(np.float64), 60_000)
+    bad, hits = run_nearest(harness, topo, pts, dirs, radii, leaf)
+    assert bad == 0 and hits > 1000
+    ang = np.linspace(0, 2 * np.pi, 401)
+    zig = np.stack([np.cos(ang) * (1 + 0.3 * (np.arange(401) % 2)), np.sin(ang) * (1 + 0.3 * (np.arange(401) % 2))], 1)
+    zig[-1] = zig[0]
+    pts, dirs, radii, _ = queries(rng, zig, 60_000)
+    # rays aimed exactly at vertices: the crossing is shared by two segments
+    k = 5000
+    j = rng.integers(1, 400, k)
+    pts[:k] = (zig[j] * 0.3).astype(np.float32)
+    dirs[:k] = (zig[j] - pts[:k]).astype(np.float32)
+    bad, hits = run_nearest(harness, zig.astype(np.float32), pts, dirs, radii, leaf)
+    assert bad == 0 and hits > 1000
