@@ -186,7 +186,7 @@ def compare_to_reference(gpu: ApparentResistivity, ref: ReferenceSurvey, replica
     error there (RMS), plus z-scores (RMS z <= 1.2, max |z| < 4). Dipoles
     the reference does not resolve are 'unpinned'.
 
-    Two 1-sigmas are reported. ref_1sigma_rms is the reference's own delta-method
+    Two 1-sigmas are reported. ref_self_reported_1sigma_rms is the reference's own delta-method
     error from its 400 walks; delta-tracking walks are heavy-tailed (the rare walks
     that cross the conductivity anomalies carry the signal), and 400 of them mostly
     miss those events, so that estimate understates the error. With ``replicas``
@@ -199,15 +199,18 @@ def compare_to_reference(gpu: ApparentResistivity, ref: ReferenceSurvey, replica
     out = {"reference_walks_per_electrode": ref.walks, "dipoles": int(len(r.rho_a)), "resolved": int(ok.sum()),
            "unpinned": int(len(r.rho_a) - ok.sum()), "reference_common_paths": ref.common_paths}
     if not ok.any():
-        out.update({"rmse": None, "ref_1sigma_rms": None, "rmse_over_1sigma": None, "z_rms": None, "z_max": None})
+        out.update({"rmse": None, "ref_self_reported_1sigma_rms": None, "rmse_over_1sigma": None, "z_rms": None,
+                    "z_max": None})
         return out
     d = gpu.rho_a[ok] - r.rho_a[ok]
     s = np.sqrt(gpu.se[ok] ** 2 + r.se[ok] ** 2)
     z = d / np.where(s > 0, s, 1.0)
     rmse = float(np.sqrt(np.mean(d * d)))
     one_sigma = float(np.sqrt(np.mean(r.se[ok] ** 2)))
-    out.update({"rmse": rmse, "ref_1sigma_rms": one_sigma,
-                "rmse_over_ref_1sigma": rmse / one_sigma if one_sigma else None,
+    # (the self-reported error of 400 heavy-tailed walks understates the MC error by
+    # orders of magnitude: kept for the record, not the north-star bound)
+    out.update({"rmse": rmse, "ref_self_reported_1sigma_rms": one_sigma,
+                "rmse_over_ref_self_reported_1sigma": rmse / one_sigma if one_sigma else None,
                 "z_rms_self_reported": float(np.sqrt(np.mean(z * z))),
                 "resolved_dipoles": [int(i) for i in np.nonzero(ok)[0]]})
     if replicas is not None:
@@ -219,7 +222,8 @@ def compare_to_reference(gpu: ApparentResistivity, ref: ReferenceSurvey, replica
                     "rmse_le_1sigma": bool(rmse <= rep_sigma), "z_rms": float(np.sqrt(np.mean(z2 * z2))),
                     "z_max": float(np.max(np.abs(z2)))})
     else:
-        out.update({"rmse_over_1sigma": out["rmse_over_ref_1sigma"], "rmse_le_1sigma": bool(rmse <= one_sigma),
+        out.update({"rmse_over_1sigma": out["rmse_over_ref_self_reported_1sigma"],
+                    "rmse_le_1sigma": bool(rmse <= one_sigma),
                     "z_rms": out["z_rms_self_reported"], "z_max": float(np.max(np.abs(z)))})
     return out
 
