@@ -1016,10 +1016,13 @@ WOST_HD Hit intersect_finish(VP v, int bi, float best, float px, float py, float
     return h;
 }
 
-// intersect_polylines_jit (:134-197).
-template <bool NORMAL = true, class VP>
+// intersect_polylines_jit (:134-197). NV > 0: a compile-time vertex count
+// (compiled-in polylines), the scan fully unrolled so the segment vectors fold.
+template <bool NORMAL = true, int NV = 0, class VP>
 WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
+    if (NV > 0) nv = NV;
+    constexpr int kUnroll = NV > 0 ? NV : 2;
     Hit h;
     float dn, dx, dy;
     unit_direction(dxi, dyi, dn, dx, dy);
@@ -1031,6 +1034,7 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
     float best = WOST_INF;
     int bi = -1;
     float2 a = v[0];
+#pragma unroll kUnroll
     for (int i = 1; i < nv; ++i) {
         float2 b = v[i];
         float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);

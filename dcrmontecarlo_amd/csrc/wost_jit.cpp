@@ -37,7 +37,8 @@ namespace {
 // alpha(z) evaluation, 16 no sigma' at collisions, 32 no Neumann ray query;
 // 64 compiled-in silhouette scans unrolled by 4 only, 128 the device library's
 // accurate sinf/cosf for the step direction instead of v_sin/v_cos; 512 no
-// whole-field saturation shortcut in the alpha jet (jet_body).
+// whole-field saturation shortcut in the alpha jet (jet_body); 1024 compiled-in
+// Neumann ray scans unrolled by 2 instead of fully.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
@@ -440,7 +441,10 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
          " float dy, float r) const {\n";
     // (a two-pass variant -- filter pass, then one exact division per lane -- measured
     // slower on C3's 32-segment circle: 1.24e10 vs 1.94e10 walk-steps/s, r02 ab_perf3)
-    if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
+    if (nconst && !(exp_flags() & 1024))   // (1024: the generic unroll-by-2 scan, A/B)
+        o << nverts_decl() << "        return wost::intersect_polylines<false, " << nn << ">(v, " << nn
+          << ", x, y, dx, dy, r);\n";
+    else if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
     else o << "        return wost::intersect_polylines<false>(sN, nn, x, y, dx, dy, r);\n";
     o << "    }\n";
     o << "    __device__ __forceinline__ float neumann_phi(const float* sPhi, int seg) const {\n";
