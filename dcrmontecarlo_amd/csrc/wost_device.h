@@ -968,9 +968,11 @@ WOST_HD Hit ray_nearest_finish(int bi, float best, float px, float py, float dx,
 // the ray, i.e. the least RAY parameter t over the segments the reference's
 // test accepts (s in [0, 1], t > 0), a hit when t <= r at q + t d. The
 // reference returns the least SEGMENT parameter instead (ray_segment_time).
-template <class VP>
+template <int NV = 0, class VP>
 WOST_HD Hit intersect_polylines_ray(VP v, int nv, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
+    if (NV > 0) nv = NV;   // compiled-in polylines: fully unrolled
+    constexpr int kUnroll = NV > 0 ? NV : 2;
     Hit h;
     float dn, dx, dy;
     unit_direction(dxi, dyi, dn, dx, dy);
@@ -982,6 +984,7 @@ WOST_HD Hit intersect_polylines_ray(VP v, int nv, float px, float py, float dxi,
     float best = WOST_INF;
     int bi = -1;
     float2 a = v[0];
+#pragma unroll kUnroll
     for (int i = 1; i < nv; ++i) {
         const float2 b = v[i];
         const float t = ray_segment_nearest_t(a, b, qx, qy, dx, dy, best);

@@ -447,6 +447,12 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     else if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
     else o << "        return wost::intersect_polylines<false>(sN, nn, x, y, dx, dy, r);\n";
     o << "    }\n";
+    o << "    __device__ __forceinline__ wost::Hit neumann_intersect_nearest(const float2* sN, int nn, float x, float y,"
+         " float dx, float dy, float r) const {\n";
+    // (the staged copy: fully unrolled over compiled-in vertices it measured no faster,
+    // profiles/r02_ab/ray_scan_full_unroll.log)
+    o << "        return wost::intersect_polylines_ray(sN, nn, x, y, dx, dy, r);\n";
+    o << "    }\n";
     o << "    __device__ __forceinline__ float neumann_phi(const float* sPhi, int seg) const {\n";
     if (nconst && nn >= 2) {
         o << "        const float phi[" << nn - 1 << "] = {";

@@ -115,6 +115,10 @@ struct InterpFields {
                                                      float r) const {
         return intersect_polylines<false>(sN, nn, x, y, dx, dy, r);
     }
+    __device__ __forceinline__ Hit neumann_intersect_nearest(const float2* sN, int nn, float x, float y, float dx,
+                                                             float dy, float r) const {
+        return intersect_polylines_ray(sN, nn, x, y, dx, dy, r);
+    }
     __device__ __forceinline__ float neumann_phi(const float* sPhi, int seg) const { return sPhi[seg]; }
 };
 

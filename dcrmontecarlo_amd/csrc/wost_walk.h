@@ -120,7 +120,8 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // alpha(x,y), alpha_jet(x,y), detached(), sigma_bar(), sqrt_sigma_bar(),
 // inv_sigma_bar(), and the polyline scans dirichlet_distance(sD,
 // nd, x, y), neumann_silhouette_distance(sN, nn, x, y), neumann_intersect(sN,
-// nn, x, y, dx, dy, r), neumann_phi(sPhi, seg) (the interpreted kernels scan the
+// nn, x, y, dx, dy, r), neumann_intersect_nearest(...) (compat="fixed"),
+// neumann_phi(sPhi, seg) (the interpreted kernels scan the
 // staged vertices; the specialised ones may have them compiled in:
 // F::kConstDirichlet / F::kConstNeumann, and then nothing is staged for them). TREE: Neumann queries through
 // the segment tree. REC: the kernel can record walks (A.rec).
@@ -368,7 +369,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
 #else
             const Hit h = FIX ? (TREE ? intersect_polylines_tree<false, true>(tree, px, py, cs, sn, r)
-                                      : intersect_polylines_ray(nP, A.nn, px, py, cs, sn, r))
+                                      : fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r))
                               : TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
                                      : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
 #endif
@@ -405,7 +406,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 yy = py + rs * sn2;
                 if (NEU)   // not visible
                     clipped = TREE ? intersect_polylines_tree<false, true>(tree, px, py, cs2, sn2, rs).hit
-                                   : intersect_polylines_ray(nP, A.nn, px, py, cs2, sn2, rs).hit;
+                                   : fld.neumann_intersect_nearest(nP, A.nn, px, py, cs2, sn2, rs).hit;
             } else {
                 // :245 (quirk Q13). FIX delta keeps the sample on the step's ray: with the
                 // nearest crossing (Q1) the clip below is exactly "y is in the star-shaped
