@@ -1266,6 +1266,23 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
         const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
         return !(b.x > b.z || fabsf(dx * cy - dy * cx) > fabsf(dx) * hy + fabsf(dy) * hx + tol);
     };
+    // A box wholly behind q (by tol + 1e-3 of its distance) holds no segment the test
+    // accepts when no segment direction of the node is within ~1e-3 rad of +-d: then
+    // |den| = |cross(d, u)| > 1e-3 |u| (the arc's edges bound it), the computed
+    // signs of den and nt are the true ones for crossings that far behind, and the
+    // test's t > 0 fails. (Near-parallel segments can be accepted with flipped signs
+    // wherever they are, so such nodes are kept.) Cone codes: 2 = only zero-length
+    // segments (never accepted), 3 = directions too spread to bound.
+    auto behind = [&](float4 b, float4 c) {
+        if (c.x == 3.0f) return false;
+        const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
+        const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
+        const float ahead = dx * cx + dy * cy + fabsf(dx) * hx + fabsf(dy) * hy;   // max over the box of (p - q) . d
+        if (!(ahead < -(tol + 1e-3f * (fabsf(cx) + fabsf(cy) + hx + hy)))) return false;
+        if (c.x == 2.0f) return true;
+        const float c1 = c.x * dy - c.y * dx, c2 = c.z * dy - c.w * dx;              // cross(e1, d), cross(e2, d)
+        return (c1 > 1e-3f && c2 > 1e-3f) || (c1 < -1e-3f && c2 < -1e-3f);
+    };
     int k = 0, depth = 0;
     uint32_t pend = 0u;   // per level: the right child is pending
     // the right child of the deepest pending level; false when nothing is pending
@@ -1282,7 +1299,13 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
         while (live && k < t.first_leaf) {
             WOST_TREE_COUNT(2);
             const float4* rr = t.record(k);
+#if defined(WOST_NO_TREE_BEHIND)
             const bool okl = line_keep(rr[0]), okr = line_keep(rr[1]);
+#else
+            const float4 b0 = rr[0], b1 = rr[1];
+            const bool okl = line_keep(b0) && !behind(b0, rr[2]);
+            const bool okr = line_keep(b1) && !behind(b1, rr[3]);
+#endif
             if (okl || okr) {
                 if (okl && okr) pend |= 1u << depth;
                 k = 2 * k + (okl ? 1 : 2);   // left first: leaves in ascending segment order

@@ -38,7 +38,8 @@ namespace {
 // 64 compiled-in silhouette scans unrolled by 4 only, 128 the device library's
 // accurate sinf/cosf for the step direction instead of v_sin/v_cos; 512 no
 // whole-field saturation shortcut in the alpha jet (jet_body); 1024 compiled-in
-// Neumann ray scans unrolled by 2 instead of fully.
+// Neumann ray scans unrolled by 2 instead of fully; 4096 the tree's ray query
+// without its behind-the-origin pruning.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
@@ -361,6 +362,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     const DField& fA = hdr.field[SLOT_ALPHA];
     std::ostringstream o;
     if (exp_flags() & 2) o << "#define WOST_EXP_IEEE_DIRECTION 1\n";
+    if (exp_flags() & 4096) o << "#define WOST_NO_TREE_BEHIND 1\n";   // A/B: line pruning only
     if (exp_flags() & 4) o << "#define WOST_ABL_NO_PHILOX 1\n";
     if (exp_flags() & 8) o << "#define WOST_ABL_NO_ALPHA_Z 1\n";
     if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
