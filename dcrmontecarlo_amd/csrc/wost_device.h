@@ -1266,19 +1266,21 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
         const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
         return !(b.x > b.z || fabsf(dx * cy - dy * cx) > fabsf(dx) * hy + fabsf(dy) * hx + tol);
     };
-    // A box wholly behind q (by tol + 1e-3 of its distance) holds no segment the test
-    // accepts when no segment direction of the node is within ~1e-3 rad of +-d: then
-    // |den| = |cross(d, u)| > 1e-3 |u| (the arc's edges bound it), the computed
-    // signs of den and nt are the true ones for crossings that far behind, and the
-    // test's t > 0 fails. (Near-parallel segments can be accepted with flipped signs
-    // wherever they are, so such nodes are kept.) Cone codes: 2 = only zero-length
-    // segments (never accepted), 3 = directions too spread to bound.
+    // A box wholly behind q holds no segment the test accepts when no segment
+    // direction of the node is within ~1e-3 rad of +-d: then |den| = |cross(d, u)| >
+    // 1e-3 |u| (|sin| over the arc is least at an edge), and a crossing behind by
+    // |t| >= 64 tol + 1e-2 L (L the box's L1 distance scale) has |nt| = |t| |den| >=
+    // 2^-8 |q| 1e-3 |u| + 1e-5 L |u|, some 30 times the rounding of nt (from q - a
+    // and the products), so the computed signs give t < 0 and the test fails.
+    // (Near-parallel segments can be accepted with flipped signs wherever they are,
+    // so such nodes are kept.) Cone codes: 2 = only zero-length segments (never
+    // accepted), 3 = directions too spread to bound.
     auto behind = [&](float4 b, float4 c) {
         if (c.x == 3.0f) return false;
         const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
         const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
         const float ahead = dx * cx + dy * cy + fabsf(dx) * hx + fabsf(dy) * hy;   // max over the box of (p - q) . d
-        if (!(ahead < -(tol + 1e-3f * (fabsf(cx) + fabsf(cy) + hx + hy)))) return false;
+        if (!(ahead < -(64.0f * tol + 1e-2f * (fabsf(cx) + fabsf(cy) + hx + hy)))) return false;
         if (c.x == 2.0f) return true;
         const float c1 = c.x * dy - c.y * dx, c2 = c.z * dy - c.w * dx;              // cross(e1, d), cross(e2, d)
         return (c1 > 1e-3f && c2 > 1e-3f) || (c1 < -1e-3f && c2 < -1e-3f);
