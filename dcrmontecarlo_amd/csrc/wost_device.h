@@ -1222,15 +1222,20 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
         const int j1 = s1 < nv - 2 ? s1 : nv - 2;
         if (s0 + 1 <= j1) {
-            float2 va = t.v[s0], vb = t.v[s0 + 1];
+            // is_silhouette with each segment's cross product formed once (vertex j's
+            // c2 is vertex j + 1's c1) and |b - x|^2 from x - b, as silhouette_distance
+            const float2 va = t.v[s0];
+            float2 vb = t.v[s0 + 1];
+            float cprev = (vb.x - va.x) * (py - va.y) - (vb.y - va.y) * (px - va.x);
             for (int j = s0 + 1; j <= j1; ++j) {
                 const float2 vc = t.v[j + 1];
-                if (is_silhouette(va, vb, vc, px, py)) {
-                    const float ex = vb.x - px, ey = vb.y - py;
-                    const float d2 = ex * ex + ey * ey;
+                const float bpx = px - vb.x, bpy = py - vb.y;
+                const float ccur = (vc.x - vb.x) * bpy - (vc.y - vb.y) * bpx;
+                if (cprev * ccur < 0.0f) {
+                    const float d2 = bpx * bpx + bpy * bpy;
                     best = d2 < best ? d2 : best;
                 }
-                va = vb;
+                cprev = ccur;
                 vb = vc;
             }
             if (best <= stop2) break;
