@@ -1099,6 +1099,16 @@ struct SegTree {
     int leaf;             // segments per leaf
     float tol;            // line-test tolerance at the origin; grows with |q|
     WOST_HD const float4* record(int k) const { return k < n_lds ? lds + 4 * k : rec + 4 * k; }
+    // word i of record k. Kernels that stage no records (all but the WOST_TREE_LDS
+    // variants, wost_jit.cpp) read them with global loads: a pointer that may point to
+    // LDS or global memory compiles to generic (flat) loads, which cost more.
+    WOST_HD float4 word(int k, int i) const {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(WOST_TREE_LDS_KERNEL)
+        return ((const __attribute__((address_space(1))) float4*)rec)[4 * k + i];
+#else
+        return record(k)[i];
+#endif
+    }
 };
 
 constexpr float kConeMargin = 1e-3f;
@@ -1182,8 +1192,7 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
             pend &= ~(1u << p);
             const int anc = ((k + 1) >> (depth - p)) - 1;
             const int side = (int)((far_right >> p) & 1u);
-            const float4* r = t.record(anc);
-            const float4 b = r[side], c = r[2 + side];
+            const float4 b = t.word(anc, side), c = t.word(anc, 2 + side);
             const float bound = best < T ? best : T;
             k = 2 * anc + 1 + side;
             depth = p + 1;
@@ -1197,8 +1206,7 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     while (live) {
         while (live && k < t.first_leaf) {
             WOST_TREE_COUNT(0);
-            const float4* r = t.record(k);
-            const float4 bl = r[0], br = r[1], cl = r[2], cr = r[3];
+            const float4 bl = t.word(k, 0), br = t.word(k, 1), cl = t.word(k, 2), cr = t.word(k, 3);
             const float bound = best < T ? best : T;
             const float lbl = box_lower_bound2(bl, px, py), lbr = box_lower_bound2(br, px, py);
             const bool okl = silhouette_keep(bl, cl, lbl, bound, px, py);
@@ -1305,13 +1313,12 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
     while (live) {                       // while-while, as in silhouette_distance_tree
         while (live && k < t.first_leaf) {
             WOST_TREE_COUNT(2);
-            const float4* rr = t.record(k);
+            const float4 b0 = t.word(k, 0), b1 = t.word(k, 1);
 #if defined(WOST_NO_TREE_BEHIND)
-            const bool okl = line_keep(rr[0]), okr = line_keep(rr[1]);
+            const bool okl = line_keep(b0), okr = line_keep(b1);
 #else
-            const float4 b0 = rr[0], b1 = rr[1];
-            const bool okl = line_keep(b0) && !behind(b0, rr[2]);
-            const bool okr = line_keep(b1) && !behind(b1, rr[3]);
+            const bool okl = line_keep(b0) && !behind(b0, t.word(k, 2));
+            const bool okr = line_keep(b1) && !behind(b1, t.word(k, 3));
 #endif
             if (okl || okr) {
                 if (okl && okr) pend |= 1u << depth;

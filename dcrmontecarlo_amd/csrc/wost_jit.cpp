@@ -39,7 +39,8 @@ namespace {
 // accurate sinf/cosf for the step direction instead of v_sin/v_cos; 512 no
 // whole-field saturation shortcut in the alpha jet (jet_body); 1024 compiled-in
 // Neumann ray scans unrolled by 2 instead of fully; 4096 the tree's ray query
-// without its behind-the-origin pruning.
+// without its behind-the-origin pruning; 8192 the tree's records through generic
+// (flat) loads in kernels that stage none.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
@@ -363,6 +364,10 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     std::ostringstream o;
     if (exp_flags() & 2) o << "#define WOST_EXP_IEEE_DIRECTION 1\n";
     if (exp_flags() & 4096) o << "#define WOST_NO_TREE_BEHIND 1\n";   // A/B: line pruning only
+    // a tree kernel that stages the tree's top records in LDS (WOST_TREE_LDS, wider
+    // workgroups) reads records through generic pointers; the others use global loads
+    if (tree && block != kWalkBlock) o << "#define WOST_TREE_LDS_KERNEL 1\n";
+    if (tree && (exp_flags() & 8192)) o << "#define WOST_TREE_LDS_KERNEL 1\n";   // A/B: flat record loads
     if (exp_flags() & 4) o << "#define WOST_ABL_NO_PHILOX 1\n";
     if (exp_flags() & 8) o << "#define WOST_ABL_NO_ALPHA_Z 1\n";
     if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
