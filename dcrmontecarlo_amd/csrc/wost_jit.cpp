@@ -298,9 +298,17 @@ const char* const kCompileOptions[] = {"-O3", "-std=c++17", "-fhip-fp32-correctl
                                        "-ffp-contract=fast-honor-pragmas"};
 constexpr int kCacheFormat = 2;   // bump when the generator or the cached file layout changes
 
+// A/B only: WOST_JIT_SCHED=<strategy> adds -mllvm -amdgpu-sched-strategy=<strategy>
+// (max-ilp, max-memory-clause, iterative-ilp, ...) to the hiprtc options.
+std::string sched_option() {
+    const char* e = std::getenv("WOST_JIT_SCHED");
+    return e && *e ? std::string("-amdgpu-sched-strategy=") + e : std::string();
+}
+
 std::string cache_identity() {
     std::string id = "fmt" + std::to_string(kCacheFormat);
     for (const char* o : kCompileOptions) id += std::string("|") + o;
+    if (!sched_option().empty()) id += "|-mllvm " + sched_option();
     int maj = 0, min = 0, rt = 0;
     if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) id += "|hiprtc" + std::to_string(maj) + "." + std::to_string(min);
     if (hipRuntimeGetVersion(&rt) == hipSuccess) id += "|hip" + std::to_string(rt);
@@ -318,6 +326,11 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
     std::string arch_opt = "--offload-arch=" + arch;
     std::vector<const char*> opts = {arch_opt.c_str()};
     for (const char* o : kCompileOptions) opts.push_back(o);
+    const std::string sched = sched_option();
+    if (!sched.empty()) {
+        opts.push_back("-mllvm");
+        opts.push_back(sched.c_str());
+    }
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
