@@ -350,13 +350,17 @@ def wenner_batches(n_electrodes: int, a: int = 1, max_sources: int = 16):
 
 
 def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, width: float = 0.5, seed: int = 0,
-                      device: int | None = None, solvers=None) -> WennerSurveyResult:
+                      device: int | None = None, solvers=None, concurrent: bool = True) -> WennerSurveyResult:
     """A Wenner-alpha line over the scenario's electrodes: transmitter
     q injects +1 A at electrode q and -1 A at q+3a (dipole_source, Gaussians of std
     `width`), receivers M = q+a, N = q+2a. Multi-source batching (wenner_batches): each
     electrode is walked once per field and its walks score the (<= 16) transmitters it
     receives, model and homogeneous background on common random numbers (the same seed
-    per group). Group g uses seed (seed, g) so that groups' walk ids stay independent."""
+    per group). Group g uses seed (seed, g) so that groups' walk ids stay independent.
+    With ``concurrent`` the model and background fields run in two host threads, each on
+    its own solver handle and HIP stream (libwost's calls release the GIL), so that two
+    launches share the GPU: a group's launch (<= 16 electrodes) under-fills it at small
+    walk counts. The results do not depend on it."""
     E = len(sc.points)
     quad = wenner_quadripoles(E, a)
     Q = len(quad)
@@ -366,17 +370,30 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
         solvers = (sm, homogeneous_solver(sc, alpha_bg, sm, device=device))
     mean = [np.full((Q, E), np.nan), np.full((Q, E), np.nan)]
     se = [np.full((Q, E), np.nan), np.full((Q, E), np.nan)]
-    steps, launches, kms = 0, 0, 0.0
-    for g, (j0, j1, t0, t1) in enumerate(wenner_batches(E, a)):
-        gseed = (int(seed) * 0x9E3779B1 + g) & (2**64 - 1)
-        for f, s in enumerate(solvers):
+    batches = list(wenner_batches(E, a))
+    acc = [[0, 0.0], [0, 0.0]]   # per field: walk-steps, walk-kernel ms
+
+    def field(f):
+        s = solvers[f]
+        for g, (j0, j1, t0, t1) in enumerate(batches):
+            gseed = (int(seed) * 0x9E3779B1 + g) & (2**64 - 1)
             _, st = s.solve_sources(sc.points[j0:j1], srcs[t0:t1], nWalks=n_walks, maxSteps=sc.max_steps, eps=sc.eps,
                                     seed=gseed, return_stats=True)
             mean[f][t0:t1, j0:j1] = st.mean
             se[f][t0:t1, j0:j1] = st.stderr
-            steps += st.total_steps
-            kms += st.kernel_ms
-        launches += 1
+            acc[f][0] += st.total_steps
+            acc[f][1] += st.kernel_ms
+
+    if concurrent:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(max_workers=2) as ex:
+            for fut in [ex.submit(field, f) for f in range(2)]:
+                fut.result()
+    else:
+        for f in range(2):
+            field(f)
+    steps, kms, launches = acc[0][0] + acc[1][0], acc[0][1] + acc[1][1], len(batches)
     q = np.arange(Q)
     M, N = quad[:, 1], quad[:, 2]
     dm = DipoleData(mean[0][q, M] - mean[0][q, N], np.sqrt(se[0][q, M] ** 2 + se[0][q, N] ** 2))
