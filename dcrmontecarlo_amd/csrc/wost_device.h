@@ -159,6 +159,32 @@ WOST_HD float f_cos(float x) { return cosf(x); }
 WOST_HD float f_log(float x) { return logf(x); }
 #endif
 
+// The correctly rounded square root (sqrtf under -fhip-fp32-correctly-rounded-
+// divide-sqrt) of a distance. The compiler's sequence is v_sqrt_f32 of x
+// (scaled by 2^32 below 2^-96), both neighbours s -+ 1 ulp tested by their
+// residuals fma(-s', s, x), the scale undone, and a class test for 0 and inf.
+// For 2^-96 <= x < inf that is exactly the four-instruction residual test on
+// x itself, written out here; other x (zero, tiny, inf, NaN, negative) take
+// sqrtf under a wave vote. Bit for bit sqrtf. WOST_EXP_IEEE_SQRT (A/B): sqrtf.
+WOST_HD float sqrt_rn(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(WOST_EXP_IEEE_SQRT)
+    const uint32_t xb = __builtin_bit_cast(uint32_t, x);
+    const bool slow = !(xb - 0x0F800000u < 0x70000000u);   // x in [2^-96, inf) as bits
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const uint32_t sb = __builtin_bit_cast(uint32_t, s);
+    const float sd = __builtin_bit_cast(float, sb - 1u), su = __builtin_bit_cast(float, sb + 1u);
+    float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
+    r = fmaf(-su, s, x) > 0.0f ? su : r;
+    if (WOST_ANY(slow)) {
+        WOST_NO_SPECULATION();
+        if (slow) r = sqrtf(x);
+    }
+    return r;
+#else
+    return sqrtf(x);
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // Fields (include/wost.h, "Coefficient fields"). A field is
 //     sum_t coef_t * prod_k factor_k(x, y)
@@ -721,7 +747,7 @@ WOST_HD float poly_distance_with(VP v, int nv, float px, float py, Div div) {
         best = d2 < best ? d2 : best;
         a = b;
     }
-    return nan ? WOST_NAN : sqrtf(best);
+    return nan ? WOST_NAN : sqrt_rn(best);
 }
 
 template <class VP>
@@ -776,7 +802,7 @@ WOST_HD float poly_distance_const(VP v, const float* rcp, int nv, float px, floa
         a = b;
     }
     redo |= !(qmin >= 0x1p-40f && qmax <= 0x1p40f);
-    float d = sqrtf(best);
+    float d = sqrt_rn(best);
     if (WOST_ANY(redo)) {
         if (redo) d = poly_distance(v, nv, px, py);
     }
@@ -827,7 +853,7 @@ WOST_HD float silhouette_distance(VP v, int nv, float px, float py) {
         cprev = ccur;
         b = c;
     }
-    return best == WOST_INF ? best : sqrtf(best);
+    return best == WOST_INF ? best : sqrt_rn(best);
 }
 
 // ray_intersection_jit (:104-132) for one segment: returns the SEGMENT
@@ -1250,7 +1276,7 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
         }
         live = resume();
     }
-    return best == WOST_INF ? best : sqrtf(best);
+    return best == WOST_INF ? best : sqrt_rn(best);
 }
 
 // intersect_polylines over the tree: the same winner as the full scan.

@@ -38,7 +38,8 @@ namespace {
 // 64 compiled-in silhouette scans unrolled by 4 only, 128 the device library's
 // accurate sinf/cosf for the step direction instead of v_sin/v_cos; 512 no
 // whole-field saturation shortcut in the alpha jet (jet_body); 1024 compiled-in
-// Neumann ray scans unrolled by 2 instead of fully; 4096 the tree's ray query
+// Neumann ray scans unrolled by 2 instead of fully; 2048 sqrtf instead of
+// sqrt_rn for the distances; 4096 the tree's ray query
 // without its behind-the-origin pruning; 8192 the tree's records through generic
 // (flat) loads in kernels that stage none.
 // Each bit only selects one fixed code path.
@@ -305,10 +306,21 @@ std::string sched_option() {
     return e && *e ? std::string("-amdgpu-sched-strategy=") + e : std::string();
 }
 
+// -fno-slp-vectorize: no packed FP32 (v_pk_*) from the SLP vectoriser. On gfx950 a
+// v_pk_{add,mul,fma}_f32 issues in the time of two scalar ones, and the pairs of
+// constants it wants in SGPRs pushed the long unrolled scans (C3's 32-segment ray
+// query, the tree traversal) past the SGPR budget into v_writelane/v_readlane
+// spills. A/B only: WOST_JIT_SLP=1 keeps the vectoriser.
+bool slp_off() {
+    const char* e = std::getenv("WOST_JIT_SLP");
+    return !(e && *e == '1');
+}
+
 std::string cache_identity() {
     std::string id = "fmt" + std::to_string(kCacheFormat);
     for (const char* o : kCompileOptions) id += std::string("|") + o;
     if (!sched_option().empty()) id += "|-mllvm " + sched_option();
+    if (slp_off()) id += "|-fno-slp-vectorize";
     int maj = 0, min = 0, rt = 0;
     if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) id += "|hiprtc" + std::to_string(maj) + "." + std::to_string(min);
     if (hipRuntimeGetVersion(&rt) == hipSuccess) id += "|hip" + std::to_string(rt);
@@ -326,6 +338,7 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
     std::string arch_opt = "--offload-arch=" + arch;
     std::vector<const char*> opts = {arch_opt.c_str()};
     for (const char* o : kCompileOptions) opts.push_back(o);
+    if (slp_off()) opts.push_back("-fno-slp-vectorize");
     const std::string sched = sched_option();
     if (!sched.empty()) {
         opts.push_back("-mllvm");
@@ -387,6 +400,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 32) o << "#define WOST_ABL_NO_RAY 1\n";
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
+    if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";

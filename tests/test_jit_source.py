@@ -12,7 +12,8 @@ from dcrmontecarlo_amd import scenarios as S
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "dcrmontecarlo_amd", "csrc")
-HIPRTC_OPTS = ["-O3", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt", "-ffp-contract=fast-honor-pragmas"]
+HIPRTC_OPTS = ["-O3", "-std=c++17", "-fhip-fp32-correctly-rounded-divide-sqrt", "-ffp-contract=fast-honor-pragmas",
+               "-fno-slp-vectorize"]
 
 
 def test_generated_sources_name_their_variant():

@@ -2,7 +2,9 @@
 """Bitwise A/B of two libwost builds: every scenario's per-walk values and step counts
 must be identical (an optimisation that claims to be exact is checked walk for walk).
 Usage (GPU box): python tools/ab_bitwise.py ab/libwost_old.so dcrmontecarlo_amd/libwost.so
-Each library runs in its own process (WOST_LIB); prints one line per scenario."""
+Each library runs in its own process (WOST_LIB); prints one line per scenario.
+A library argument may carry environment settings for its process:
+lib.so:WOST_JIT_SLP=1 (several joined by commas)."""
 import json
 import os
 import subprocess
@@ -36,9 +38,11 @@ def main():
         run_one(sys.argv[2])
         return
     outs = []
-    for i, lib in enumerate(sys.argv[1:3]):
+    for i, arg in enumerate(sys.argv[1:3]):
+        lib, _, extra = arg.partition(":")
         out = os.path.join(REPO, "gpurun_out", f"ab_bitwise_{i}.npz")
         env = dict(os.environ, WOST_LIB=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
         subprocess.run([sys.executable, os.path.abspath(__file__), "--one", out], check=True, env=env)
         outs.append(np.load(out))
     ok_all = True

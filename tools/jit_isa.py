@@ -38,6 +38,7 @@ def main():
     asm = os.path.join(a.out, f"{a.scenario}.s")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "--offload-device-only", "-S", "-O3", "-std=c++17",
            "-fhip-fp32-correctly-rounded-divide-sqrt", "-ffp-contract=fast-honor-pragmas",
+           *([] if os.environ.get("WOST_JIT_SLP") == "1" else ["-fno-slp-vectorize"]),
            "-I", os.path.join(REPO, "include"), "-I", os.path.join(REPO, "dcrmontecarlo_amd", "csrc"), hip, "-o", asm]
     subprocess.run(cmd, check=True)
     text = open(asm).read()
