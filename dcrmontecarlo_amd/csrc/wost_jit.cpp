@@ -401,6 +401,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
+    if (const char* e = std::getenv("WOST_JIT_REFILL_MIN"))   // A/B: refill batch size
+        o << "#define WOST_REFILL_MIN " << std::max(1, std::min(64, std::atoi(e))) << "\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";

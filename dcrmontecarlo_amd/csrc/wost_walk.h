@@ -163,6 +163,9 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // GL: the polylines (and segment angles) are read from global memory instead of being
 // staged in LDS -- field-specialised kernels for polylines too long for the LDS budget
 // (wost_api.hip kGlobalPolylineLdsBytes).
+#ifndef WOST_REFILL_MIN   // idle lanes that trigger a refill (tools/ab_refill.sh; 1 = every iteration)
+#define WOST_REFILL_MIN 4
+#endif
 template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, bool FIX = false, bool GL = false,
           class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
@@ -257,8 +260,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             active = false;
         }
 
-        // --- refill idle lanes from the wave's chunk (active-mask compaction)
+        // --- refill idle lanes from the wave's chunk (active-mask compaction), in
+        // batches: the refill runs on the few lanes it starts while the wave's other
+        // lanes wait, so finished lanes idle until WOST_REFILL_MIN of them (or all
+        // the wave's live ones) can start together. Each walk's result depends only
+        // on its id, so the batching changes no bits.
         uint64_t need = __ballot(!active);
+        if (__popcll(need) < WOST_REFILL_MIN && __any(active)) need = 0ull;
         while (need != 0ull && !exhausted) {
             if (c_next >= c_end) {
                 unsigned long long c = 0;
