@@ -242,9 +242,18 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #pragma unroll
     for (int s = 0; s < NS; ++s) total[s] = 0.f;
 
+    // Tree kernels (long walks) also defer a finished walk's end record and output
+    // into the refill batch: it idles until WOST_REFILL_MIN lanes are finished or
+    // idle, or no lane is still stepping (C5 +4%; C3 and Laplace -2%, C4 neutral:
+    // profiles/r02_ab/termination_batch.log). Its state does not change meanwhile,
+    // so neither do its bits.
+    constexpr bool kBatchEnd = TREE;
     for (;;) {
+        const bool done = active && !((k < A.max_steps) && (dD > A.eps));
+        bool batch = true;
+        if (kBatchEnd) batch = __popcll(__ballot(done || !active)) >= WOST_REFILL_MIN || !__any(active && !done);
         // --- walk termination: while-condition of :206, boundary term :295-298
-        if (active && !((k < A.max_steps) && (dD > A.eps))) {
+        if (batch && done) {
             float g = fld.has_g() ? fld.g(px, py) : 0.0f;
             if (DELTA) g = g * w;
 #pragma unroll
@@ -265,8 +274,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         // lanes wait, so finished lanes idle until WOST_REFILL_MIN of them (or all
         // the wave's live ones) can start together. Each walk's result depends only
         // on its id, so the batching changes no bits.
-        uint64_t need = __ballot(!active);
-        if (__popcll(need) < WOST_REFILL_MIN && __any(active)) need = 0ull;
+        uint64_t need = batch ? __ballot(!active) : 0ull;
+        if (!kBatchEnd && __popcll(need) < WOST_REFILL_MIN && __any(active)) need = 0ull;
         while (need != 0ull && !exhausted) {
             if (c_next >= c_end) {
                 unsigned long long c = 0;
