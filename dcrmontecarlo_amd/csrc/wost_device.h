@@ -1073,6 +1073,46 @@ WOST_HD Hit intersect_polylines(VP v, int nv, float px, float py, float dxi, flo
     return intersect_finish<NORMAL>(v, bi, best, px, py, dx, dy, qx, qy, r);
 }
 
+// intersect_polylines over compiled-in vertices v (NV <= 65) in two passes: the
+// unrolled filter of ray_segment_time_filtered marks each lane's candidate segments
+// in a bit mask, then each lane decides only its own candidates, in ascending order,
+// with the same function on the staged copy sv (so `s < best` keeps the first
+// argmin): the per-segment exact tests no longer run for the whole wave whenever
+// one lane has a candidate there. Bit for bit intersect_polylines.
+template <int NV, class VP, class SP>
+WOST_HD Hit intersect_polylines_compact(VP v, SP sv, float px, float py, float dxi, float dyi, float r) {
+#pragma clang fp contract(off)
+    static_assert(NV >= 2 && NV <= 65, "one bit per segment");
+    Hit h;
+    float dn, dx, dy;
+    unit_direction(dxi, dyi, dn, dx, dy);
+    if (dn < 1e-10f) {
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
+        return h;
+    }
+    const float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
+    uint64_t cand = 0ull;
+#pragma unroll
+    for (int i = 1; i < NV; ++i) {
+        const float2 a = v[i - 1], b = v[i];
+        const float ux = b.x - a.x, uy = b.y - a.y;
+        const float wx = qx - a.x, wy = qy - a.y;
+        const float den = dx * uy - dy * ux;
+        const float rd = f_rcp(den);
+        const float sa = (dx * wy - dy * wx) * rd, ta = (ux * wy - uy * wx) * rd;
+        if (sa >= -1e-6f && sa <= 1.000001f && ta >= 0.0f) cand |= 1ull << (i - 1);
+    }
+    float best = WOST_INF;
+    int bi = -1;
+    while (cand != 0ull) {
+        const int j = __builtin_ctzll(cand);
+        cand &= cand - 1ull;
+        const float s = ray_segment_time_filtered(sv[j], sv[j + 1], qx, qy, dx, dy);
+        if (s < best) { best = s; bi = j; }
+    }
+    return intersect_finish<false>(v, bi, best, px, py, dx, dy, qx, qy, r);
+}
+
 // ---------------------------------------------------------------------------
 // Segment tree over a long Neumann polyline (topography with 10^4+ segments).
 // The reference scans every segment at every step (PolylinesSimple.py:83-102,

@@ -41,7 +41,8 @@ namespace {
 // Neumann ray scans unrolled by 2 instead of fully; 2048 sqrtf instead of
 // sqrt_rn for the distances; 4096 the tree's ray query
 // without its behind-the-origin pruning; 8192 the tree's records through generic
-// (flat) loads in kernels that stage none.
+// (flat) loads in kernels that stage none; 16384 the per-segment exact tests instead
+// of the two-pass scan (intersect_polylines_compact) for 8+ compiled-in segments.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
@@ -475,9 +476,13 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    }\n";
     o << "    __device__ __forceinline__ wost::Hit neumann_intersect(const float2* sN, int nn, float x, float y, float dx,"
          " float dy, float r) const {\n";
-    // (a two-pass variant -- filter pass, then one exact division per lane -- measured
-    // slower on C3's 32-segment circle: 1.24e10 vs 1.94e10 walk-steps/s, r02 ab_perf3)
-    if (nconst && !(exp_flags() & 1024))   // (1024: the generic unroll-by-2 scan, A/B)
+    // (a two-pass variant with one exact division per lane and a rescan on near ties
+    // measured slower on C3's 32-segment circle: 1.24e10 vs 1.94e10 walk-steps/s)
+    // 8+ compiled-in segments: the two-pass scan (C3's 32-segment circle +11%; with one or
+    // two segments its loop costs more than it saves: C4 -9%, profiles/r02_ab/ray_scan_two_pass.log)
+    if (nconst && nn >= 9 && nn <= 65 && !(exp_flags() & 16384))   // (16384: per-segment exact tests, A/B)
+        o << nverts_decl() << "        return wost::intersect_polylines_compact<" << nn << ">(v, sN, x, y, dx, dy, r);\n";
+    else if (nconst && !(exp_flags() & 1024))   // (1024: the generic unroll-by-2 scan, A/B)
         o << nverts_decl() << "        return wost::intersect_polylines<false, " << nn << ">(v, " << nn
           << ", x, y, dx, dy, r);\n";
     else if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
