@@ -16,7 +16,19 @@ electrode. --scaling weak (default): W = N x 1M, so each GPU keeps the one-GPU
 workload; --scaling strong: W = 1M split N ways. The communicator's id travels
 through the launcher's TCP store; no torch process group is created.
 
+--workload wenner_topography (BASELINE configs[4]): the 256-electrode
+Wenner-alpha line over the 10,000-segment topography, model and homogeneous
+background, every electrode's walks scoring the (<= 16) transmitters it receives
+(survey.run_wenner_survey); one bench step = one whole survey. N ranks shard every
+group's walks by walk range (comm.solve_sources_distributed, one communicator per
+field so the two fields run concurrently); weak scaling keeps --walks per electrode
+per GPU. Its cpu_baseline is the oracle's brute-force scan (the reference's
+algorithm), and the segment tree's gain is reported as speedup_vs_bruteforce
+against the device's own brute-force scan kernel (never as a roofline
+fraction).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
+                       [--workload dcr_dipole|wenner_topography]
        (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 Prints one JSON line on rank 0.
 """
@@ -39,8 +51,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--walks", type=int, default=1_000_000, help="walks per electrode")
-    ap.add_argument("--electrodes", type=int, default=48)
+    ap.add_argument("--workload", choices=["dcr_dipole", "wenner_topography"], default="dcr_dipole")
+    ap.add_argument("--walks", type=int, default=None,
+                    help="walks per electrode per GPU (dcr_dipole 1M, wenner_topography 100k)")
+    ap.add_argument("--literal", action="store_true",
+                    help="wenner_topography: the notebook's conductivity with its air term (default: the "
+                         "physical variant without it, so rho_a is meaningful)")
+    ap.add_argument("--no-bruteforce", action="store_true", help="wenner_topography: skip the scan-kernel leg")
+    ap.add_argument("--electrodes", type=int, default=None, help="dcr_dipole 48, wenner_topography 256")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: N x --walks walks per electrode on N GPUs (default); strong: --walks on N GPUs")
@@ -154,7 +172,24 @@ def reference_leg(survey, alpha_bg, vm, vh):
     return out
 
 
-def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu, paired=None):
+def replay_leg(survey, solver, solver_h):
+    """Deterministic rho_a parity: the reference's survey replayed on the Philox stream
+    (tests/golden/rho_replay_dcr_dipole.npz, all 48 electrodes, model + background) and
+    the device on the same walks -- step counts, per-walk values and every dipole's
+    paired rho_a, independent of Monte-Carlo error."""
+    ref = survey.load_replay_survey(os.path.join(REPO, "tests", "golden", "rho_replay_dcr_dipole.npz"))
+    if ref is None:
+        return None
+    kw = dict(nWalks=ref.n_walks, maxSteps=ref.max_steps, eps=ref.eps, seed=ref.seed)
+    vm, sm = solver.solve_walks(ref.points, **kw)
+    vh, sh = solver_h.solve_walks(ref.points, **kw)
+    out = survey.compare_to_replay(vm, vh, sm, sh, ref)
+    out.pop("rho_a_reference")
+    out.pop("rho_a_gpu")
+    return out
+
+
+def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu, paired=None, replay=None):
     """Apparent resistivity of the dipole-dipole line: the full GPU run's precision, the
     full GPU run against the reference's own run (tests/golden/rho_dcr_dipole.npz: the
     north-star RMSE <= 1 sigma check), and the GPU vs the CPU port (oracle) on the same
@@ -173,8 +208,12 @@ def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu, paired=Non
            "gpu_full": {"walks_per_electrode": int(gpu_full[2]), "resolved": int(ok.sum()),
                         "mc_1sigma_rms": float(np.sqrt(np.mean(full.se[ok] ** 2))) if ok.any() else None,
                         "rho_a_checksum": float(np.sum(full.rho_a[ok]))}}
+    if replay is not None:
+        out["vs_reference_replay"] = replay
     if paired is not None:
-        out["vs_reference"] = reference_leg(survey, alpha_bg, *paired)
+        # statistical leg against the reference's own RNG: its replica bound is the spread
+        # of the GPU's own 400-walk estimates (the reference's stated error understates it)
+        out["vs_reference_statistical"] = reference_leg(survey, alpha_bg, *paired)
     if cpu_same is not None:
         g, c = rho(*gpu_same), rho(*cpu_same)
         cmp = survey.compare(g, c)
@@ -221,6 +260,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload == "wenner_topography":
+        return wenner_main(args, world, rank, local)
+    args.walks = args.walks or 1_000_000
+    args.electrodes = args.electrodes or 48
 
     from dcrmontecarlo_amd import comm as C
     from dcrmontecarlo_amd import perfmodel
@@ -351,11 +394,154 @@ def main():
             st_m, st_h = stats_from_sums(last_sums, Wt), stats_from_sums(sums_h, Wt)
             gpu_full = ((st_m.mean, st_m.stderr), (st_h.mean, st_h.stderr), Wt)
             paired = paired_walks(survey, sc, solver, solver_h, RHO_REPLICA_WALKS * RHO_REPLICAS)
-            out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu, paired)
+            replay = replay_leg(survey, solver, solver_h) if len(sc.points) == 48 else None
+            out["rho_a"] = rho_report(survey, ALPHA_BG, gpu_full, gpu_same, cpu_same, w_cpu, paired, replay)
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.barrier()
         comm.close()
+
+
+WENNER_ALPHA_BG = 1e-2     # notebook cell 17's background conductivity (rho_bg = 100)
+WENNER_ISSUE = "profiles/issue_wenner_topography.json"
+
+
+def wenner_cpu_leg(sc, sigma_bar, budget_s):
+    """The oracle's brute-force scan (the reference's algorithm: every segment, twice
+    per step) on a bounded sample of the C5 survey's walks, one source field, on every
+    usable core; then on one core."""
+    from oracle import oracle as O
+
+    info = host_cpu()
+    threads = info["affinity_cpus"]
+    if info["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(round(info["cgroup_cpu_quota"]))))
+    pb = O.Problem.from_scenario(sc, sigma_bar=sigma_bar)
+    pts = sc.points[::8]                                   # 32 electrodes along the line
+    pb.solve_walks(pts[:1], 1, sc.max_steps, sc.eps, 1, threads=1)
+    w = 2
+    while True:
+        t0 = time.perf_counter()
+        _, s = pb.solve_walks(pts, w, sc.max_steps, sc.eps, CPU_SEED, threads=threads)
+        dt = time.perf_counter() - t0
+        if dt >= 0.4 * budget_s or w >= 100_000:
+            break
+        w = int(min(100_000, w * max(2.0, 0.8 * budget_s / max(dt, 1e-3))))
+    base = {"value": float(s.sum()) / dt, "unit": "walk-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{sc.name}: {len(pts)} electrodes x {w} walks, one source field ({int(s.sum())} walk-steps, "
+                      f"{dt:.1f} s); oracle/wost_oracle.c brute-force scans of the {len(sc.neumann) - 1}-segment "
+                      f"topography, {threads} OpenMP threads (every usable host core)",
+            "host": info}
+    t0 = time.perf_counter()
+    _, s1 = pb.solve_walks(pts[:4], max(1, w // 4), sc.max_steps, sc.eps, CPU_SEED + 1, threads=1)
+    dt1 = time.perf_counter() - t0
+    base["single_core"] = {"value": float(s1.sum()) / dt1, "cores": 1,
+                           "sample": f"4 electrodes x {max(1, w // 4)} walks ({int(s1.sum())} walk-steps, {dt1:.1f} s)"}
+    return base
+
+
+def wenner_main(args, world, rank, local):
+    """BASELINE configs[4] / SURVEY C5 (module docstring)."""
+    from dcrmontecarlo_amd import comm as C
+    from dcrmontecarlo_amd import perfmodel
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd import survey
+
+    W1 = args.walks or 100_000
+    E = args.electrodes or 256
+    sc = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=not args.literal)
+    sm = sc.solver(device=local)
+    sh = survey.homogeneous_solver(sc, WENNER_ALPHA_BG, sm, device=local)
+    comms = None
+    if world > 1 or os.environ.get("WOST_BENCH_FORCE_COMM"):
+        cm = C.Communicator.from_env(device=local)
+        ch = C.Communicator.from_env(device=local, key="wost_comm_uid_background", store=getattr(cm, "_store", None))
+        comms = (cm, ch)
+    Wt = W1 * (world if args.scaling == "weak" else 1)
+    w0, w1 = C.shard_walk_range(Wt, world, rank)
+
+    def step(seed, walks=Wt):
+        return survey.run_wenner_survey(sc, WENNER_ALPHA_BG, walks, seed=seed, solvers=(sm, sh), comm=comms)
+
+    def barrier():
+        if comms is not None:
+            comms[0].barrier()
+
+    for k in range(args.warmup):
+        step(1000 + k)
+    barrier()
+    t0 = time.perf_counter()
+    steps_all, steps_local, kernel_ms, res = 0, 0, 0.0, None
+    for k in range(args.steps):
+        res = step(k)
+        steps_all += int(res.walk_steps)           # all ranks' walk-steps (solve_sources_distributed)
+        steps_local += int(res.local_walk_steps)   # this rank's
+        kernel_ms += float(res.kernel_ms)          # this rank's walk-kernel time, both fields
+    barrier()
+    elapsed = time.perf_counter() - t0
+    max_elapsed = elapsed if comms is None else float(comms[0].allreduce([elapsed], "max")[0])
+
+    if rank == 0:
+        value = steps_all / max_elapsed
+        kernel_rate = steps_local / (kernel_ms * 1e-3) if kernel_ms > 0 else 0.0   # both fields' kernels summed
+        ok = res.rho.resolved & np.isfinite(res.rho.rho_a)
+        out = {
+            "metric": "walk-steps/sec", "value": value, "unit": "walk-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * max_elapsed / args.steps,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (notebook cell 17 fields, 10k-segment y = 1 + 2 sin(x/37) topography, Philox4x32-10)",
+            "config": {"workload": f"{sc.name}: BASELINE configs[4] / SURVEY 8d C5 -- Wenner-alpha line, {E} "
+                                   f"electrodes, {len(sc.neumann) - 1}-segment Neumann topography, model + "
+                                   f"homogeneous background, multi-source batched (<= 16 transmitters per walk)",
+                       "electrodes": E, "quadripoles": int(len(res.quadripoles)),
+                       "walks_per_electrode": Wt, "walks_per_electrode_per_gpu": w1 - w0,
+                       "launches_per_field": res.launches, "walk_steps_per_survey": steps_all // max(args.steps, 1),
+                       "parallelism": (f"walk-range shards of every electrode over {world} GPUs "
+                                       "(comm.solve_sources_distributed: libwost RCCL all-gather of block sums, "
+                                       "one communicator per field)") if world > 1 else "one GPU"},
+            "kernel_walk_steps_per_s": kernel_rate,
+        }
+        roof = {"bound": "valu-issue", "unit": "SIMD cycles/s", "traffic": None,
+                "note": "SURVEY 8d: the segment tree is never priced as a FLOP roofline fraction; this is the "
+                        "VALU issue-rate line from committed PMC passes, and speedup_vs_bruteforce below"}
+        try:
+            with open(os.path.join(REPO, WENNER_ISSUE)) as f:
+                pmc = json.load(f)
+            roof.update(perfmodel.issue_fraction(pmc["valu_per_wave_step"], pmc["trans_per_wave_step"], kernel_rate))
+            roof.update({"achieved": roof["achieved_simd_cycles_per_s"], "peak": roof["peak_simd_cycles_per_s"],
+                         "lane_utilisation": pmc.get("lane_utilisation"), "pmc_source": pmc.get("source")})
+        except (OSError, ValueError, KeyError):
+            roof.update({"achieved": None, "peak": perfmodel.N_SIMDS * perfmodel.CLOCK_GHZ * 1e9, "frac": None})
+        out["roofline"] = roof
+        if not args.no_bruteforce:
+            # the device's brute-force scan kernel (the reference's algorithm, every segment twice
+            # per step) on a chip-filling sample: 256 electrodes x 2048 walks, one source
+            bf = sc.solver(device=local)
+            bf.set_segment_tree(-1)
+            nb = min(E, 256)
+            _, st = bf.solve(sc.points[:nb], nWalks=2048, maxSteps=sc.max_steps, eps=sc.eps, seed=5,
+                             return_stats=True)
+            rate_bf = st.total_steps / (st.kernel_ms * 1e-3)
+            bs = perfmodel.flops_per_step(sc)      # SURVEY 8d v1, brute force (~290,000 FLOP/step)
+            out["speedup_vs_bruteforce"] = {
+                "bruteforce_kernel_walk_steps_per_s": rate_bf, "tree_kernel_walk_steps_per_s": kernel_rate,
+                "speedup": kernel_rate / rate_bf if rate_bf > 0 else None,
+                "bruteforce_sample": f"{nb} electrodes x 2048 walks, one source, scan kernel",
+                "bruteforce_model_tflops": rate_bf * bs / 1e12,
+                "bruteforce_frac_fp32": rate_bf * bs / 1e12 / perfmodel.FP32_PEAK_TFLOPS}
+        out["cpu_baseline"] = (wenner_cpu_leg(sc, sm.sigma_bar or 0.0, args.cpu_seconds)
+                               if (not args.no_cpu and world == 1) else None)
+        out["rho_a"] = {"array": f"Wenner-alpha a = 1, {len(res.quadripoles)} quadripoles", "rho_bg": 1 / WENNER_ALPHA_BG,
+                        "resolved": int(ok.sum()),
+                        "median": float(np.median(res.rho.rho_a[ok])) if ok.any() else None,
+                        "p10_p90": [float(np.percentile(res.rho.rho_a[ok], q)) for q in (10, 90)] if ok.any() else None,
+                        "mc_1sigma_rms": float(np.sqrt(np.mean(res.rho.se[ok] ** 2))) if ok.any() else None,
+                        "rho_a_checksum": float(np.sum(res.rho.rho_a[ok]))}
+        print(json.dumps(out), flush=True)
+    if comms is not None:
+        comms[0].barrier()
+        for c in comms:
+            c.close()
 
 
 if __name__ == "__main__":

@@ -69,6 +69,18 @@ class WostDistTiming(ctypes.Structure):
     _fields_ = [("local", WostTiming), ("walk_begin", c_int64), ("walk_end", c_int64), ("total_steps", c_uint64)]
 
 
+DIST_PREPARE = ctypes.CFUNCTYPE(c_int32, c_void_p, c_int64)
+DIST_SOLVE_RANGE = ctypes.CFUNCTYPE(c_int32, c_void_p, c_int64, c_int64, POINTER(c_double))
+DIST_ALLREDUCE = ctypes.CFUNCTYPE(c_int32, c_void_p, POINTER(c_double), c_int64, c_int32)
+DIST_ALLGATHER = ctypes.CFUNCTYPE(c_int32, c_void_p, POINTER(c_double), c_int64, POINTER(c_double))
+
+
+class WostDistOps(ctypes.Structure):
+    """include/wost.h wost_dist_ops: the transport of wost_distributed_run."""
+    _fields_ = [("ctx", c_void_p), ("prepare", DIST_PREPARE), ("solve_range", DIST_SOLVE_RANGE),
+                ("allreduce", DIST_ALLREDUCE), ("allgather", DIST_ALLGATHER)]
+
+
 class WostError(RuntimeError):
     """A libwost call failed (HIP error, no device, out of memory)."""
 
@@ -114,6 +126,13 @@ def _load():
         "wost_shard_walk_range": (c_int32, [c_int64, c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
         "wost_solve_distributed": (c_int32, [H, c_void_p, POINTER(c_float), c_int64, c_int64, c_int32, c_float,
                                              c_uint64, POINTER(c_double), POINTER(WostDistTiming)]),
+        "wost_shard_blocks_max": (c_int64, [c_int64, c_int32]),
+        "wost_shard_pack": (c_int32, [POINTER(c_double), c_int64, c_int64, c_int32, c_int32, c_int32,
+                                      POINTER(c_double)]),
+        "wost_shard_merge": (c_int32, [POINTER(c_double), c_int64, c_int64, c_int32, c_int32, POINTER(c_double)]),
+        "wost_distributed_run": (c_int32, [POINTER(WostDistOps), c_int32, c_int32, c_int64, c_int64, c_int32,
+                                           POINTER(c_double), POINTER(c_int64), POINTER(c_int64),
+                                           POINTER(c_uint64)]),
         "wost_greens_norm": (c_int32, [c_double, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_screened_sample_fixed": (c_int32, [POINTER(c_float), POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_screened_cdf_fixed": (c_int32, [c_double, POINTER(c_double), c_int64, POINTER(c_double)]),

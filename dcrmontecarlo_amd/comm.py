@@ -30,7 +30,7 @@ def shard_walk_range(walks_per_point: int, n_ranks: int, rank: int) -> tuple[int
     return min(b0 * _lib.WOST_BLOCK_WALKS, walks_per_point), min(b1 * _lib.WOST_BLOCK_WALKS, walks_per_point)
 
 
-def exchange_over_store(make_id, key: str = "wost_comm_uid", timeout: float = 300.0):
+def exchange_over_store(make_id, key: str = "wost_comm_uid", timeout: float = 300.0, store=None):
     """Rank 0 publishes make_id() under `key` in the TCP store at MASTER_ADDR:MASTER_PORT,
     every rank reads it back: (bytes, store). Under torchrun's elastic agent the store
     already listens on MASTER_PORT (TORCHELASTIC_USE_AGENT_STORE) and every rank joins
@@ -42,8 +42,9 @@ def exchange_over_store(make_id, key: str = "wost_comm_uid", timeout: float = 30
 
     rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
     agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
-    store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
-                          is_master=(rank == 0 and not agent), timeout=timedelta(seconds=timeout))
+    if store is None:   # (a second id -- a second communicator -- reuses the first one's store)
+        store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
+                              is_master=(rank == 0 and not agent), timeout=timedelta(seconds=timeout))
     k = f"{key}/{os.environ.get('TORCHELASTIC_RUN_ID', '')}/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
     if rank == 0:
         store.set(k, make_id())
@@ -82,16 +83,18 @@ class Communicator:
         return cls(box[0], world, rank, device)
 
     @classmethod
-    def from_env(cls, device: int | None = None, key: str = "wost_comm_uid", timeout: float = 300.0) -> "Communicator":
+    def from_env(cls, device: int | None = None, key: str = "wost_comm_uid", timeout: float = 300.0,
+                 store=None) -> "Communicator":
         """Bootstrap from the torchrun environment (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR,
         MASTER_PORT) without a torch process group: the id travels through a TCP
-        key-value store (exchange_over_store)."""
+        key-value store (exchange_over_store). A further communicator over the same
+        ranks passes its own ``key`` and the first one's ``_store``."""
         rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         if world == 1 and "MASTER_PORT" not in os.environ:   # a lone process: no store needed
             return cls(unique_id(), 1, 0, device)
-        uid, store = exchange_over_store(unique_id, key, timeout)
+        uid, store = exchange_over_store(unique_id, key, timeout, store)
         c = cls(uid, world, rank, device)
         c._store = store   # keep the store (and, on rank 0, its server) alive with the communicator
         return c
@@ -135,24 +138,20 @@ class Communicator:
         return out
 
     def allreduce(self, a, op: str = "sum") -> np.ndarray:
+        ops = {"sum": _lib.WOST_COMM_SUM, "max": _lib.WOST_COMM_MAX}
+        if op not in ops:
+            raise ValueError(f"allreduce op must be 'sum' or 'max', got {op!r}")
         a = np.array(a, np.float64, copy=True, ndmin=1)
-        _lib.check(_lib.lib.wost_comm_allreduce(self._c, _lib.dptr(a), a.size,
-                                                _lib.WOST_COMM_SUM if op == "sum" else _lib.WOST_COMM_MAX),
-                   "wost_comm_allreduce", comm=True)
+        _lib.check(_lib.lib.wost_comm_allreduce(self._c, _lib.dptr(a), a.size, ops[op]), "wost_comm_allreduce",
+                   comm=True)
         return a
 
     def barrier(self):
         _lib.check(_lib.lib.wost_comm_barrier(self._c), "wost_comm_barrier", comm=True)
 
 
-def solve_distributed(solver, comm: Communicator, points, nWalks: int, maxSteps: int = 1000, eps: float = 1e-4,
-                      seed: int = 0):
-    """WostSolver_2D.solve across the communicator's ranks (collective; every rank passes
-    the same arguments). Returns (u [N,1] float32, SolveStats, timing dict) on every rank;
-    u and the statistics are bitwise those of a one-GPU solve."""
-    from .solvers.WoStSolver import stats_from_sums
-
-    p = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 2))
+def _distributed_sums(solver, comm: Communicator, p: np.ndarray, nWalks: int, maxSteps: int, eps: float,
+                      seed: int):
     n = p.shape[0]
     ns = ctypes.c_int32(1)
     _lib.check(_lib.lib.wost_num_sources(solver._h, ctypes.byref(ns)), "wost_num_sources")
@@ -165,5 +164,47 @@ def solve_distributed(solver, comm: Communicator, points, nWalks: int, maxSteps:
     timing.update({"walk_begin": int(t.walk_begin), "walk_end": int(t.walk_end), "all_steps": int(t.total_steps)})
     solver.last_timing = timing
     solver.last_point_sums = sums
-    st = stats_from_sums(sums[:, [0, 1, -1]] if sums.shape[1] > 3 else sums, int(nWalks))
-    return st.mean.astype(np.float32).reshape(n, 1), st, timing
+    return sums, timing
+
+
+def solve_distributed(solver, comm: Communicator, points, nWalks: int, maxSteps: int = 1000, eps: float = 1e-4,
+                      seed: int = 0):
+    """WostSolver_2D.solve across the communicator's ranks (collective; every rank passes
+    the same arguments). Returns (u [N,1] float32, SolveStats, timing dict) on every rank;
+    u and the statistics are bitwise those of a one-GPU solve. Multi-source solves go
+    through solve_sources_distributed."""
+    from .solvers.WoStSolver import stats_from_sums
+
+    p = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 2))
+    sums, timing = _distributed_sums(solver, comm, p, nWalks, maxSteps, eps, seed)
+    if sums.shape[1] != 3:
+        raise ValueError("the solver scores several sources: use solve_sources_distributed")
+    st = stats_from_sums(sums, int(nWalks), timing["all_steps"], timing["walk_kernel_ms"], timing["total_ms"])
+    return st.mean.astype(np.float32).reshape(p.shape[0], 1), st, timing
+
+
+def solve_sources_distributed(solver, comm: Communicator, points, sources, nWalks: int, maxSteps: int = 1000,
+                              eps: float = 1e-4, seed: int = 0):
+    """WostSolver_2D.solve_sources across the communicator's ranks (collective): every
+    source scored by the same walks, the walk ranges sharded as in solve_distributed.
+    Returns (u [S, N] float32, SolveStats with [S, N] mean / stderr, timing dict) on
+    every rank, bitwise those of a one-GPU solve_sources."""
+    from .solvers.WoStSolver import SolveStats, _stats_of_multi
+
+    p = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 2))
+    fields = solver.source_fields(sources)
+    stats, steps, lsteps, kms, tms = [], 0, 0, 0.0, 0.0
+    for c0 in range(0, len(fields), _lib.WOST_MAX_SOURCES):
+        with solver.sources_installed(fields[c0:c0 + _lib.WOST_MAX_SOURCES]):
+            sums, timing = _distributed_sums(solver, comm, p, nWalks, maxSteps, eps, seed)
+        stats.extend(_stats_of_multi(sums, int(nWalks)))
+        steps += timing["all_steps"]
+        lsteps += timing["total_steps"]
+        kms += timing["walk_kernel_ms"]
+        tms += timing["total_ms"]
+    timing = dict(timing, all_steps=steps, total_steps=lsteps, walk_kernel_ms=kms, total_ms=tms)
+    solver.last_timing = timing
+    u = np.stack([st.mean.astype(np.float32) for st in stats])
+    return u, SolveStats(mean=np.stack([st.mean for st in stats]), stderr=np.stack([st.stderr for st in stats]),
+                         mean_steps=stats[0].mean_steps, walks=int(nWalks), total_steps=steps, kernel_ms=kms,
+                         total_ms=tms), timing

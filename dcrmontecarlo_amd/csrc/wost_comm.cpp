@@ -174,59 +174,188 @@ int wost_shard_walk_range(int64_t walks_per_point, int32_t n_ranks, int32_t rank
     return WOST_OK;
 }
 
-int wost_solve_distributed(wost_handle* h, wost_comm* c, const float* points, int64_t n_points,
-                           int64_t walks_per_point, int32_t max_steps, float eps, uint64_t seed, double* point_stats,
-                           wost_dist_timing* timing) {
-    if (!h || !c || !point_stats || n_points < 0 || (n_points > 0 && !points) || walks_per_point < 1)
-        return cfail(WOST_ERR_INVALID_ARG, "bad arguments");
-    double sb = 0.0;
-    int32_t delta = 0;
-    (void)wost_get_info(h, &sb, &delta);
-    int32_t ns = 1;
-    if (wost_num_sources(h, &ns) != WOST_OK) return cfail(WOST_ERR_INVALID_ARG, "%s", wost_last_error());
-    const int row = 2 * ns + 1;
-    const int R = c->n_ranks;
+int64_t wost_shard_blocks_max(int64_t walks_per_point, int32_t n_ranks) {
+    if (walks_per_point < 1 || n_ranks < 1) return -1;
     const int64_t nbpp = (walks_per_point + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
-    const int64_t nb_max = (nbpp + R - 1) / R;   // blocks per point of the largest shard
-    std::fill(point_stats, point_stats + (size_t)row * (size_t)n_points, 0.0);
-    if (n_points == 0) return WOST_OK;
+    return (nbpp + n_ranks - 1) / n_ranks;   // blocks per point of the largest shard
+}
+
+int wost_shard_pack(const double* blocks, int64_t n_points, int64_t walks_per_point, int32_t n_ranks, int32_t rank,
+                    int32_t row, double* packed) {
     int64_t w0 = 0, w1 = 0;
-    int rc = wost_shard_walk_range(walks_per_point, R, c->rank, &w0, &w1);
-    if (rc != WOST_OK) return rc;
-    // this rank's blocks, padded to nb_max per point for the all-gather
-    std::vector<double> mine((size_t)n_points * (size_t)nb_max * (size_t)row, 0.0);
-    wost_timing t{};
-    if (w1 > w0) {
-        const int64_t nbr = (w1 - w0 + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
-        std::vector<double> bs((size_t)n_points * (size_t)nbr * (size_t)row);
-        rc = wost_solve_range(h, points, n_points, walks_per_point, w0, w1, max_steps, eps, seed, bs.data(), nullptr,
-                              nullptr, nullptr);
-        if (rc != WOST_OK) return cfail(rc, "%s", wost_last_error());
-        (void)wost_last_timing(h, &t);
-        for (int64_t p = 0; p < n_points; ++p)
-            std::memcpy(&mine[((size_t)p * nb_max) * row], &bs[((size_t)p * nbr) * row], sizeof(double) * nbr * row);
-    }
-    std::vector<double> all((size_t)R * mine.size());
-    rc = wost_comm_allgather(c, mine.data(), (int64_t)mine.size(), all.data());
-    if (rc != WOST_OK) return rc;
+    if (n_points < 0 || row < 1 || !packed || (n_points > 0 && !blocks && walks_per_point > 0) ||
+        wost_shard_walk_range(walks_per_point, n_ranks, rank, &w0, &w1) != WOST_OK)
+        return cfail(WOST_ERR_INVALID_ARG, "wost_shard_pack: bad arguments");
+    const int64_t nb_max = wost_shard_blocks_max(walks_per_point, n_ranks);
+    const int64_t nbr = w1 > w0 ? (w1 - w0 + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS : 0;
+    std::fill(packed, packed + (size_t)n_points * (size_t)nb_max * (size_t)row, 0.0);
+    for (int64_t p = 0; p < n_points; ++p)
+        if (nbr) std::memcpy(&packed[(size_t)p * nb_max * row], &blocks[(size_t)p * nbr * row], sizeof(double) * nbr * row);
+    return WOST_OK;
+}
+
+int wost_shard_merge(const double* gathered, int64_t n_points, int64_t walks_per_point, int32_t n_ranks, int32_t row,
+                     double* point_stats) {
+    const int64_t nb_max = wost_shard_blocks_max(walks_per_point, n_ranks);
+    if (nb_max < 0 || n_points < 0 || row < 1 || !point_stats || (n_points > 0 && !gathered))
+        return cfail(WOST_ERR_INVALID_ARG, "wost_shard_merge: bad arguments");
+    const size_t per_rank = (size_t)n_points * (size_t)nb_max * (size_t)row;
+    std::fill(point_stats, point_stats + (size_t)n_points * (size_t)row, 0.0);
     // per point, every rank's blocks in rank order = the global block order of one GPU
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < n_ranks; ++r) {
         int64_t a0 = 0, a1 = 0;
-        (void)wost_shard_walk_range(walks_per_point, R, r, &a0, &a1);
+        (void)wost_shard_walk_range(walks_per_point, n_ranks, r, &a0, &a1);
         const int64_t nbr = a1 > a0 ? (a1 - a0 + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS : 0;
-        const double* part = &all[(size_t)r * mine.size()];
+        const double* part = gathered + (size_t)r * per_rank;
         for (int64_t p = 0; p < n_points; ++p)
             for (int64_t b = 0; b < nbr; ++b)
                 for (int k = 0; k < row; ++k) point_stats[(size_t)p * row + k] += part[((size_t)p * nb_max + b) * row + k];
     }
+    return WOST_OK;
+}
+
+int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank, int64_t n_points,
+                         int64_t walks_per_point, int32_t row, double* point_stats, int64_t* walk_begin,
+                         int64_t* walk_end, uint64_t* total_steps) {
+    if (!ops || !ops->allreduce || !ops->allgather || n_ranks < 1 || rank < 0 || rank >= n_ranks)
+        return cfail(WOST_ERR_INVALID_ARG, "wost_distributed_run: no transport or bad rank %d of %d", rank, n_ranks);
+    // Every rank reaches the same two collectives, whatever fails locally: the
+    // agreement all-reduce (MAX) carries a failure flag and the call's shape, and
+    // only when no rank failed and all agree does the all-gather of the blocks run.
+    int local = WOST_OK;
+    std::string local_msg;
+    int64_t w0 = 0, w1 = 0;
+    const bool args_ok = point_stats && n_points >= 0 && walks_per_point >= 1 && row >= 1 && ops->solve_range;
+    if (!args_ok) {
+        local = WOST_ERR_INVALID_ARG;
+        local_msg = "bad arguments";
+    } else {
+        (void)wost_shard_walk_range(walks_per_point, n_ranks, rank, &w0, &w1);
+    }
+    const int64_t nb_max = args_ok ? wost_shard_blocks_max(walks_per_point, n_ranks) : 0;
+    const int64_t nbr = w1 > w0 ? (w1 - w0 + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS : 0;
+    const size_t per_rank = args_ok ? (size_t)n_points * (size_t)nb_max * (size_t)row : 0;
+    std::vector<double> mine, all;
+    if (local == WOST_OK) {
+        try {
+            mine.assign(per_rank, 0.0);
+            all.assign(per_rank * (size_t)n_ranks, 0.0);
+        } catch (const std::bad_alloc&) {
+            local = WOST_ERR_OOM;
+            local_msg = "host buffers of the gather";
+        }
+    }
+    if (local == WOST_OK && ops->prepare) {
+        local = ops->prepare(ops->ctx, (int64_t)per_rank);
+        if (local != WOST_OK) local_msg = "transport buffers: " + g_comm_err;
+    }
+    if (local == WOST_OK && n_points > 0 && nbr > 0) {
+        std::vector<double> bs;
+        try {
+            bs.assign((size_t)n_points * (size_t)nbr * (size_t)row, 0.0);
+        } catch (const std::bad_alloc&) {
+            local = WOST_ERR_OOM;
+            local_msg = "host block buffer";
+        }
+        if (local == WOST_OK) {
+            local = ops->solve_range(ops->ctx, w0, w1, bs.data());
+            if (local != WOST_OK) local_msg = "local solve: " + g_comm_err;
+        }
+        if (local == WOST_OK) (void)wost_shard_pack(bs.data(), n_points, walks_per_point, n_ranks, rank, row, mine.data());
+    }
+    // agreement: max of (failed, n_points, -n_points, row, -row, W, -W)
+    double agree[7] = {local != WOST_OK ? 1.0 : 0.0, (double)n_points, -(double)n_points, (double)row, -(double)row,
+                       (double)walks_per_point, -(double)walks_per_point};
+    int rc = ops->allreduce(ops->ctx, agree, 7, WOST_COMM_MAX);
+    if (rc != WOST_OK) return cfail(rc, "agreement all-reduce: %s", g_comm_err.c_str());
+    if (local != WOST_OK) return cfail(local, "rank %d: %s", rank, local_msg.c_str());
+    if (agree[0] > 0.0) return cfail(WOST_ERR_COMM, "rank %d: another rank failed; no result", rank);
+    if (agree[1] != -agree[2] || agree[3] != -agree[4] || agree[5] != -agree[6])
+        return cfail(WOST_ERR_INVALID_ARG, "ranks disagree on the solve (n_points %g..%g, row %g..%g, walks %g..%g)",
+                     -agree[2], agree[1], -agree[4], agree[3], -agree[6], agree[5]);
+    if (per_rank > 0) {
+        rc = ops->allgather(ops->ctx, mine.data(), (int64_t)per_rank, all.data());
+        if (rc != WOST_OK) return cfail(rc, "block all-gather: %s", g_comm_err.c_str());
+    }
+    rc = wost_shard_merge(all.data(), n_points, walks_per_point, n_ranks, row, point_stats);
+    if (rc != WOST_OK) return rc;
+    if (walk_begin) *walk_begin = w0;
+    if (walk_end) *walk_end = w1;
+    if (total_steps) {
+        double s = 0.0;
+        for (int64_t p = 0; p < n_points; ++p) s += point_stats[(size_t)p * row + row - 1];
+        *total_steps = (uint64_t)s;
+    }
+    return WOST_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// wost_solve_distributed's transport: RCCL on the communicator's stream, and the
+// handle's wost_solve_range as the local solve
+struct RcclRun {
+    wost_handle* h;
+    wost_comm* c;
+    const float* points;
+    int64_t n_points, walks_per_point;
+    int32_t max_steps;
+    float eps;
+    uint64_t seed;
+    wost_timing t{};
+};
+
+int32_t rccl_prepare(void* ctx, int64_t per_rank) {
+    auto* r = static_cast<RcclRun*>(ctx);
+    CHIP_TRY(hipSetDevice(r->c->device));
+    return ensure_comm_buffers(r->c, std::max<int64_t>(per_rank, 8));
+}
+
+int32_t rccl_solve_range(void* ctx, int64_t w0, int64_t w1, double* blocks) {
+    auto* r = static_cast<RcclRun*>(ctx);
+    const int rc = wost_solve_range(r->h, r->points, r->n_points, r->walks_per_point, w0, w1, r->max_steps, r->eps,
+                                    r->seed, blocks, nullptr, nullptr, nullptr);
+    if (rc != WOST_OK) return cfail(rc, "%s", wost_last_error());
+    (void)wost_last_timing(r->h, &r->t);
+    return WOST_OK;
+}
+
+int32_t rccl_allreduce(void* ctx, double* inout, int64_t count, int32_t op) {
+    return wost_comm_allreduce(static_cast<RcclRun*>(ctx)->c, inout, count, op);
+}
+
+int32_t rccl_allgather(void* ctx, const double* send, int64_t count, double* recv) {
+    return wost_comm_allgather(static_cast<RcclRun*>(ctx)->c, send, count, recv);
+}
+
+}  // namespace
+
+extern "C" {
+
+int wost_solve_distributed(wost_handle* h, wost_comm* c, const float* points, int64_t n_points,
+                           int64_t walks_per_point, int32_t max_steps, float eps, uint64_t seed, double* point_stats,
+                           wost_dist_timing* timing) {
+    if (!c) return cfail(WOST_ERR_INVALID_ARG, "NULL communicator");
+    // local argument and handle problems go through the agreement collective
+    // (wost_distributed_run), so that no rank is left waiting in the gather
+    int32_t ns = 1;
+    int32_t row = 3;
+    if (!h || wost_num_sources(h, &ns) != WOST_OK) row = 0;
+    else row = 2 * ns + 1;
+    if (n_points > 0 && !points) row = 0;
+    RcclRun run{h, c, points, n_points, walks_per_point, max_steps, eps, seed};
+    wost_dist_ops ops{&run, rccl_prepare, rccl_solve_range, rccl_allreduce, rccl_allgather};
+    int64_t w0 = 0, w1 = 0;
+    uint64_t steps = 0;
+    const int rc = wost_distributed_run(&ops, c->n_ranks, c->rank, n_points, walks_per_point, row, point_stats, &w0,
+                                        &w1, &steps);
+    if (rc != WOST_OK) return rc;
     if (timing) {
-        timing->local = t;
+        timing->local = run.t;
         timing->walk_begin = w0;
         timing->walk_end = w1;
-        double steps = (double)t.total_steps;
-        rc = wost_comm_allreduce(c, &steps, 1, WOST_COMM_SUM);
-        if (rc != WOST_OK) return rc;
-        timing->total_steps = (uint64_t)steps;
+        timing->total_steps = steps;
     }
     return WOST_OK;
 }

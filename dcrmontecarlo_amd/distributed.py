@@ -6,11 +6,14 @@ every point, one all-gather of the block sums, per-point sums in global block
 order -- bitwise the one-GPU result). This module holds the host-side mirror of
 that merge (merge_walk_range_blocks, block_stats_of_walks: the gloo CPU tests
 drive real shards of oracle walks through it), the weak-scaling replication
-helpers of bench.py, and an optional torch.distributed path (contiguous block
-ranges, all_gather of the rows through torch's backend) for callers that
-already run a torch process group.
+helpers of bench.py, and the torch.distributed path: libwost's own protocol
+(wost_distributed_run -- the code wost_solve_distributed runs over RCCL) with
+torch's collectives as its transport, for callers that already run a torch
+process group, and for the gloo CPU tests of that protocol.
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 
@@ -113,18 +116,116 @@ def merge_replicas(sums: np.ndarray, world: int) -> np.ndarray:
     return acc
 
 
+class _Transport:
+    """Python callables behind a wost_dist_ops (include/wost.h): libwost's own
+    distributed protocol (wost_distributed_run) drives them. An exception in a
+    callback becomes an error status for the protocol (and is re-raised by
+    run_protocol on the rank where it happened)."""
+
+    def __init__(self, n_points, row, solve_range, allreduce, allgather, prepare=None):
+        from . import _lib
+
+        self.error = None
+        self.n_points, self.row = int(n_points), int(row)
+
+        def guard(fn):
+            def wrapped(*a):
+                try:
+                    return fn(*a)
+                except Exception as e:   # noqa: BLE001 -- reported through the protocol
+                    if self.error is None:
+                        self.error = e
+                    return _lib.WOST_ERR_COMM
+            return wrapped
+
+        def _solve(ctx, w0, w1, blocks):
+            nbr = -(-(int(w1) - int(w0)) // _lib.WOST_BLOCK_WALKS)
+            b = np.ascontiguousarray(solve_range(int(w0), int(w1)), np.float64)
+            if b.shape != (self.n_points, nbr, self.row):
+                raise ValueError(f"solve_range returned {b.shape}, expected {(self.n_points, nbr, self.row)}")
+            ctypes.memmove(blocks, b.ctypes.data, b.nbytes)
+            return 0
+
+        def _allreduce(ctx, ptr, count, op):
+            a = np.ctypeslib.as_array(ptr, shape=(int(count),))
+            a[:] = allreduce(a.copy(), "sum" if op == _lib.WOST_COMM_SUM else "max")
+            return 0
+
+        def _allgather(ctx, send, count, recv):
+            a = np.ctypeslib.as_array(send, shape=(int(count),)).copy()
+            out = np.ascontiguousarray(allgather(a), np.float64).ravel()
+            r = np.ctypeslib.as_array(recv, shape=(out.size,))
+            r[:] = out
+            return 0
+
+        def _prepare(ctx, count):
+            if prepare is not None:
+                prepare(int(count))
+            return 0
+
+        self._cb = (_lib.DIST_PREPARE(guard(_prepare)), _lib.DIST_SOLVE_RANGE(guard(_solve)),
+                    _lib.DIST_ALLREDUCE(guard(_allreduce)), _lib.DIST_ALLGATHER(guard(_allgather)))
+        self.ops = _lib.WostDistOps(None, *self._cb)
+
+
+def run_protocol(n_ranks: int, rank: int, n_points: int, walks_per_point: int, row: int, solve_range, allreduce,
+                 allgather, prepare=None):
+    """libwost's distributed protocol (wost_distributed_run: agreement all-reduce,
+    all-gather of the padded block rows, ordered merge) over Python callables:
+    solve_range(w0, w1) -> [n_points, blocks, row] float64 of this rank's walks;
+    allreduce(a, "sum"|"max") -> a reduced; allgather(a) -> [n_ranks, a.size].
+    Returns (point sums [n_points, row], (walk_begin, walk_end), total walk-steps).
+    Raises the local exception on the rank whose callback failed, WostError on the
+    others (no rank is left waiting in a collective)."""
+    from . import _lib
+
+    tr = _Transport(n_points, row, solve_range, allreduce, allgather, prepare)
+    out = np.zeros((int(n_points), int(row)), np.float64)
+    w0, w1, steps = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_uint64()
+    rc = _lib.lib.wost_distributed_run(ctypes.byref(tr.ops), int(n_ranks), int(rank), int(n_points),
+                                       int(walks_per_point), int(row), _lib.dptr(out), ctypes.byref(w0),
+                                       ctypes.byref(w1), ctypes.byref(steps))
+    if rc != _lib.WOST_OK and tr.error is not None:
+        raise tr.error
+    _lib.check(rc, "wost_distributed_run", comm=True)
+    return out, (int(w0.value), int(w1.value)), int(steps.value)
+
+
+def torch_transport(group=None, device=None):
+    """(allreduce, allgather) over a torch.distributed group (gloo on CPU; with
+    ``device`` a CUDA device, the nccl/RCCL backend)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    dev = device or "cpu"
+
+    def allreduce(a, op):
+        t = torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX, group=group)
+        return t.cpu().numpy()
+
+    def allgather(a):
+        t = torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(dev)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t, group=group)
+        return np.stack([o.cpu().numpy() for o in outs])
+
+    return allreduce, allgather
+
+
 def solve_distributed(solver, points, nWalks: int, maxSteps: int = 1000, eps: float = 1e-4, seed: int = 0,
                       group=None, device=None):
     """WostSolver_2D.solve across the ranks of ``group`` (torch.distributed must be
-    initialised). Returns (u [N,1] float32, SolveStats) on every rank."""
+    initialised): libwost's walk-range protocol (wost_distributed_run) with torch's
+    collectives as the transport. Returns (u [N,1] float32, SolveStats) on every
+    rank, bitwise those of a one-GPU solve."""
     import torch.distributed as dist
 
     pts = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 2))
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    nb = solver.num_blocks(pts.shape[0], nWalks)
-    b0, b1 = shard_range(nb, rank, world)
-    local = solver.solve_blocks(pts, nWalks, b0, b1, maxSteps, eps, seed)
-    allb = gather_block_stats(local, nb, group, device)
-    sums = point_sums(allb, pts.shape[0])
+    ar, ag = torch_transport(group, device)
+    sums, _, steps = run_protocol(world, rank, pts.shape[0], int(nWalks), 3,
+                                  lambda w0, w1: solver.solve_range(pts, nWalks, w0, w1, maxSteps, eps, seed), ar, ag)
     u = (sums[:, 0] / nWalks).astype(np.float32).reshape(-1, 1)
-    return u, stats_from_sums(sums, nWalks)
+    return u, stats_from_sums(sums, nWalks, steps)

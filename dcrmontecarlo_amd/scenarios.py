@@ -161,12 +161,15 @@ def dcr_reference_electrodes() -> np.ndarray:
     return np.stack([x, np.zeros_like(x)], axis=1)
 
 
-def notebook_alpha() -> F.Field:
-    """conductivity_field_torch, tests/testNotebook.ipynb cell 17."""
-    bg, air = 1e-2, 1e-8
-    return (bg + (1e-1 - bg) * F.smooth_circle((-120.0, -80.0), 60.0)
-            + (1e-3 - bg) * F.smooth_circle((120.0, -80.0), 60.0)
-            + (air - bg) * F.sigmoid(10000.0 * Y))
+def notebook_alpha(air: bool = True) -> F.Field:
+    """conductivity_field_torch, tests/testNotebook.ipynb cell 17. ``air=False`` drops
+    its air term (alpha = 1e-8 above y = 0): over a topographic Neumann surface that
+    rises to y = 3, the term would put surface electrodes in "air"; the zero-flux
+    surface already models the air."""
+    bg, air_v = 1e-2, 1e-8
+    a = (bg + (1e-1 - bg) * F.smooth_circle((-120.0, -80.0), 60.0)
+         + (1e-3 - bg) * F.smooth_circle((120.0, -80.0), 60.0))
+    return a + (air_v - bg) * F.sigmoid(10000.0 * Y) if air else a
 
 
 def notebook_source() -> F.Field:
@@ -192,15 +195,25 @@ def topography(n_segments: int = 10_000) -> np.ndarray:
     return np.stack([x, 1.0 + 2.0 * np.sin(x / 37.0)], axis=1).astype(np.float32)
 
 
-def wenner_topography(n_electrodes: int = 256, n_walks: int = 10_000, n_segments: int = 10_000) -> Scenario:
-    """C5: notebook fields and U boundary with a 10k-segment topographic Neumann surface."""
+def wenner_topography(n_electrodes: int = 256, n_walks: int = 10_000, n_segments: int = 10_000,
+                      physical: bool = False) -> Scenario:
+    """C5: notebook fields and U boundary with a 10k-segment topographic Neumann surface.
+    The literal variant keeps the notebook's conductivity, air term included (the
+    parity workload); ``physical=True`` (wenner_topography_physical) drops the air
+    term, which is flat at y = 0 while the surface rises to y = 3, so that the
+    electrodes sit in the ground and the apparent resistivities mean something."""
     D = np.array([[-500.0, 1.0], [-500.0, -1000.0], [500.0, -1000.0], [500.0, 1.0]], np.float32)
     N = topography(n_segments)
     x = np.linspace(-400.0, 400.0, n_electrodes).astype(np.float32)
     y = (1.0 + 2.0 * np.sin(x.astype(np.float64) / 37.0) - 0.1).astype(np.float32)
-    return Scenario("wenner_topography", D, N, g=F.const(0.0), f=notebook_source(), sigma=None, alpha=notebook_alpha(),
+    return Scenario("wenner_topography_physical" if physical else "wenner_topography", D, N, g=F.const(0.0),
+                    f=notebook_source(), sigma=None, alpha=notebook_alpha(air=not physical),
                     points=np.stack([x, y], axis=1), n_walks=n_walks, max_steps=500, eps=0.9,
                     reference="SURVEY.md 8d C5 (notebook cells 17-18 + synthetic topography)")
+
+
+def wenner_topography_physical(n_electrodes: int = 256, n_walks: int = 10_000, n_segments: int = 10_000) -> Scenario:
+    return wenner_topography(n_electrodes, n_walks, n_segments, physical=True)
 
 
 ALL = {
@@ -211,4 +224,5 @@ ALL = {
     "dcr_dipole": dcr_dipole,
     "notebook_dcr": notebook_dcr,
     "wenner_topography": wenner_topography,
+    "wenner_topography_physical": wenner_topography_physical,
 }

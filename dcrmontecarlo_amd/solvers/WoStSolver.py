@@ -22,6 +22,7 @@ Differences a caller sees:
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 from dataclasses import dataclass
@@ -368,25 +369,40 @@ class WostSolver_2D:
         return wv.reshape(n, nWalks), ws.reshape(n, nWalks)
 
     # ---- multi-source batching -------------------------------
+    def source_fields(self, sources) -> list:
+        """The device fields of a list of sources (fields, numbers or callables; None = 0)."""
+        srcs = list(sources)
+        if not srcs:
+            raise ValueError("sources must hold at least one source field")
+        return [self._conv(0.0 if f is None else f, f"sources[{k}]") for k, f in enumerate(srcs)]
+
+    @contextlib.contextmanager
+    def sources_installed(self, fields):
+        """Score up to WOST_MAX_SOURCES source fields per walk (wost_set_sources) inside
+        the block; the solver's own (single) source is restored afterwards."""
+        if not 1 <= len(fields) <= _lib.WOST_MAX_SOURCES:
+            raise ValueError(f"1..{_lib.WOST_MAX_SOURCES} sources per launch, got {len(fields)}")
+        packed = [_lib.make_field(f) for f in fields]
+        arr = (ctypes.POINTER(_lib.WostField) * len(fields))(*[ctypes.pointer(wf) for wf, _ in packed])
+        _lib.check(_lib.lib.wost_set_sources(self._h, arr, len(fields)), "WostSolver_2D.solve_sources")
+        try:
+            yield len(fields)
+        finally:
+            wf, keep = _lib.make_field(self.source)
+            _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_SOURCE, ctypes.pointer(wf) if wf else None),
+                       "WostSolver_2D.solve_sources")
+
     def _solve_sources(self, solvePoints, sources, nWalks, maxSteps, eps, seed, want_walks):
         p = _points_np(solvePoints)
         n = p.shape[0]
         nWalks = int(nWalks)
         if nWalks < 1:
             raise ValueError("nWalks must be >= 1")
-        srcs = list(sources)
-        if not srcs:
-            raise ValueError("sources must hold at least one source field")
-        fields = [self._conv(0.0 if f is None else f, f"sources[{k}]") for k, f in enumerate(srcs)]
+        fields = self.source_fields(sources)
         nb = self.num_blocks(n, nWalks)
         sums, vals, steps = [], [], None
-        try:
-            for c0 in range(0, len(fields), _lib.WOST_MAX_SOURCES):
-                chunk = fields[c0:c0 + _lib.WOST_MAX_SOURCES]
-                S = len(chunk)
-                packed = [_lib.make_field(f) for f in chunk]
-                arr = (ctypes.POINTER(_lib.WostField) * S)(*[ctypes.pointer(wf) for wf, _ in packed])
-                _lib.check(_lib.lib.wost_set_sources(self._h, arr, S), "WostSolver_2D.solve_sources")
+        for c0 in range(0, len(fields), _lib.WOST_MAX_SOURCES):
+            with self.sources_installed(fields[c0:c0 + _lib.WOST_MAX_SOURCES]) as S:
                 s = np.zeros((n, 2 * S + 1), np.float64)
                 wv = np.empty(n * nWalks * S, np.float32) if want_walks else None
                 ws = np.empty(n * nWalks, np.uint32) if want_walks else None
@@ -394,14 +410,10 @@ class WostSolver_2D:
                                                      float(eps), int(seed) & (2**64 - 1), None, _lib.dptr(s),
                                                      _lib.fptr(wv), _lib.u32ptr(ws)), "WostSolver_2D.solve_sources")
                 self.last_timing = self.timing()
-                sums.append(s)
-                if want_walks:
-                    vals.append(wv.reshape(n, nWalks, S).transpose(2, 0, 1))
-                    steps = ws.reshape(n, nWalks)
-        finally:   # back to the solver's own (single) source
-            wf, keep = _lib.make_field(self.source)
-            _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_SOURCE, ctypes.pointer(wf) if wf else None),
-                       "WostSolver_2D.solve_sources")
+            sums.append(s)
+            if want_walks:
+                vals.append(wv.reshape(n, nWalks, S).transpose(2, 0, 1))
+                steps = ws.reshape(n, nWalks)
         return sums, vals, steps
 
     def solve_sources(self, solvePoints, sources, nWalks=1000, maxSteps=1000, eps=1e-4, *, seed: int = 0,

@@ -315,6 +315,51 @@ int wost_solve_distributed(wost_handle* h, wost_comm* c, const float* points, in
                            int64_t walks_per_point, int32_t max_steps, float eps, uint64_t seed,
                            double* point_stats, wost_dist_timing* timing);
 
+/* The pieces of wost_solve_distributed, host only (no device needed), so that the
+ * multi-rank merge and the failure protocol run under any transport -- RCCL in
+ * wost_solve_distributed, gloo in the CPU tests.
+ *
+ * Layout of one rank's contribution to the all-gather: [n_points][nb_max][row]
+ * doubles, nb_max = wost_shard_blocks_max(W, n_ranks), the rank's blocks of each
+ * point first and zero padding after them (row = 2S+1 block sums). */
+int64_t wost_shard_blocks_max(int64_t walks_per_point, int32_t n_ranks);
+/* blocks [n_points][n_rank_blocks][row] of rank `rank`'s walk range -> packed. */
+int wost_shard_pack(const double* blocks, int64_t n_points, int64_t walks_per_point, int32_t n_ranks,
+                    int32_t rank, int32_t row, double* packed);
+/* gathered [n_ranks][n_points][nb_max][row] -> point_stats [n_points][row]: per point,
+ * rank 0's blocks, then rank 1's, ... added to 0.0 one block at a time -- the block
+ * order of a one-GPU solve, so the sums are bitwise the same for any n_ranks. */
+int wost_shard_merge(const double* gathered, int64_t n_points, int64_t walks_per_point, int32_t n_ranks,
+                     int32_t row, double* point_stats);
+
+/* A transport for wost_distributed_run. Every callback returns WOST_OK or an error
+ * status (and may set its message with nothing: the protocol records its own).
+ *   prepare      optional: reserve transport buffers for `count` doubles per rank
+ *   solve_range  this rank's walks [walk_begin, walk_end) of every point ->
+ *                blocks [n_points][n_rank_blocks][row] (wost_solve_range's layout)
+ *   allreduce    inout[count] reduced over ranks, op WOST_COMM_SUM / WOST_COMM_MAX
+ *   allgather    recv[n_ranks][count] = every rank's send[count], in rank order */
+typedef struct {
+    void* ctx;
+    int32_t (*prepare)(void* ctx, int64_t count);
+    int32_t (*solve_range)(void* ctx, int64_t walk_begin, int64_t walk_end, double* blocks);
+    int32_t (*allreduce)(void* ctx, double* inout, int64_t count, int32_t op);
+    int32_t (*allgather)(void* ctx, const double* send, int64_t count, double* recv);
+} wost_dist_ops;
+
+/* The distributed solve's protocol over a transport (collective). Every rank makes
+ * exactly two collective calls, in the same order, whatever fails locally:
+ *   1. allreduce(MAX) of (failed, n_points, row, walks_per_point) -- so a rank whose
+ *      solve or buffers failed, or whose arguments differ, is known to all;
+ *   2. only if no rank failed and all agree: allgather of the packed blocks,
+ *      then wost_shard_merge.
+ * A rank that failed returns its own status; the others return WOST_ERR_COMM
+ * ("another rank failed"); disagreeing shapes give WOST_ERR_INVALID_ARG on all.
+ * walk_begin / walk_end / total_steps (all ranks' walk-steps) may be NULL. */
+int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank, int64_t n_points,
+                         int64_t walks_per_point, int32_t row, double* point_stats,
+                         int64_t* walk_begin, int64_t* walk_end, uint64_t* total_steps);
+
 /* Walk kernels: by default libwost compiles a field-specialised walk kernel per
  * handle and kernel variant with hiprtc (cached in memory and in
  * $WOST_JIT_CACHE, default ~/.cache/wost) and falls back to the precompiled

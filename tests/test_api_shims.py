@@ -89,3 +89,26 @@ def test_cross_product_2d_broadcasts_like_the_reference():
     assert torch.equal(got, want)
     single = poly.crossProduct2D(np.array([1.0, 0.0], np.float32), np.array([0.0, 1.0], np.float32))
     assert np.asarray(single).ravel()[0] == 1.0
+
+
+def test_utils_autograd_helpers_and_plot_stubs():
+    """The root utils shim's host helpers (reference utils.py:11-120): gradient,
+    Laplacian with its +1e-8 offset, grid min/max; the plotting functions (out of
+    scope) raise NotImplementedError instead of failing on import."""
+    import utils
+
+    p = torch.tensor([1.0, 2.0])
+    g = utils.torchGradient(lambda x: x[0] ** 2 + 3 * x[1], p)
+    assert g.tolist() == [2.0, 3.0]
+    assert float(utils.torchLaplacian(lambda x: x[0] ** 4 + x[1] ** 4, p)) == pytest.approx(60.0)
+    # a linear function: its gradient has no graph, the second derivative raises and
+    # the 1e-8 offset comes back (the reference's silent fallback)
+    assert float(utils.torchLaplacian(lambda x: x[0] + 2 * x[1], p)) == pytest.approx(1e-8, rel=1e-6)
+    lo, hi, plo, phi = utils.gridSampleMinMax(lambda x: (x[0] - 0.5) ** 2 + x[1] ** 2, [[0.0, 1.0], [0.0, 1.0]], 11)
+    assert lo == pytest.approx(0.0) and hi == pytest.approx(1.25)
+    assert plo.tolist() == pytest.approx([0.5, 0.0]) and phi.tolist() == pytest.approx([0.0, 1.0])
+    with pytest.raises(ValueError):
+        utils.gridSampleMinMax(lambda x: x[0] / 0.0 * 0.0, [[0.0, 1.0]], 5)
+    for name in ("plot_walk_history", "plot_multiple_walks", "plot_walk_statistics"):
+        with pytest.raises(NotImplementedError):
+            getattr(utils, name)({})

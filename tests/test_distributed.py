@@ -1,6 +1,9 @@
-"""Multi-rank reduction (dcrmontecarlo_amd.distributed) with the gloo backend on CPU,
-world_size 2 and 3: shards partition the blocks, the all_gather reassembles them
-in block order, and the per-point sums are bitwise identical to one rank's."""
+"""Multi-rank reduction with the gloo backend on CPU, world_size 2 and 3: shards
+partition the blocks, the all_gather reassembles them in block order, and the
+per-point sums are bitwise identical to one rank's. The merge and the failure
+protocol are libwost's own C++ (wost_shard_pack / wost_shard_merge /
+wost_distributed_run, the code wost_solve_distributed runs over RCCL), driven
+here through gloo with oracle walk shards; no device is needed."""
 import os
 import socket
 
@@ -201,3 +204,154 @@ def test_communicator_id_travels_through_the_launch_store(agent):
         assert p.exitcode == 0
     assert all(res[r] == bytes(range(128)) for r in range(world))
     del host
+
+
+# ---------------------------------------------------------------- libwost's C++ merge and protocol
+def _lib_pack_merge(parts_blocks, W, R, row):
+    """Pack every rank's blocks with wost_shard_pack, concatenate (the all-gather's
+    layout) and merge with wost_shard_merge."""
+    from dcrmontecarlo_amd import _lib
+
+    n = parts_blocks[0].shape[0]
+    nb_max = int(_lib.lib.wost_shard_blocks_max(W, R))
+    gathered = np.zeros((R, n, nb_max, row))
+    for r in range(R):
+        b = np.ascontiguousarray(parts_blocks[r], np.float64)
+        out = np.empty((n, nb_max, row))
+        assert _lib.lib.wost_shard_pack(_lib.dptr(b), n, W, R, r, row, _lib.dptr(out)) == 0
+        gathered[r] = out
+    sums = np.empty((n, row))
+    assert _lib.lib.wost_shard_merge(_lib.dptr(gathered), n, W, R, row, _lib.dptr(sums)) == 0
+    return sums
+
+
+@pytest.mark.parametrize("row", [3, 7])
+@pytest.mark.parametrize("W", [1, 4096, 3 * 4096 + 1000, 11 * 4096, 20 * 4096 + 1])
+def test_library_merge_equals_mirror_and_one_rank(W, row):
+    """wost_shard_pack + wost_shard_merge (the C++ of wost_solve_distributed) for
+    R in {2, 3, 8}, ragged last shards, empty shards (R > blocks) and multi-source
+    rows (2S+1 = 7): bitwise equal to the host mirror and to one rank's sums."""
+    rng = np.random.default_rng(W + row)
+    n = 5
+    nb = -(-W // 4096)
+    full = rng.standard_normal((n, nb, row)) * np.array([1e3, 1e-7, 1e6, 3.0, 1.0, 7.0, 4096.0][:row])
+    one = _lib_pack_merge([full], W, 1, row)
+    acc = np.zeros((n, row))
+    for b in range(nb):      # one GPU: blocks of a point added to 0.0 in order
+        acc += full[:, b]
+    assert np.array_equal(one, acc)
+    for R in (2, 3, 8):
+        parts = []
+        for r in range(R):
+            w0, w1 = D.shard_walk_range(W, R, r)
+            b0, b1 = w0 // 4096, -(-w1 // 4096) if w1 > w0 else w0 // 4096
+            parts.append(full[:, b0:b1])
+        got = _lib_pack_merge(parts, W, R, row)
+        assert np.array_equal(got, acc), R
+        assert np.array_equal(got, D.merge_walk_range_blocks(
+            [np.pad(p, ((0, 0), (0, max(0, -(-nb // R) - p.shape[1])), (0, 0))) for p in parts], W))
+
+
+def _protocol_worker(rank, world, port, W, mode, out_q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd import _lib
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = S.poisson_square()
+    pts = sc.points[:3]
+    ar, ag = D.torch_transport()
+
+    myW = W + 4096 if (mode == "disagree" and rank == 1) else W
+
+    def solve_range(w0, w1):
+        if mode == "fail" and rank == world - 1:
+            raise RuntimeError("injected failure")
+        return _oracle_range_blocks(sc, pts, myW, w0, w1, 99)
+
+    try:
+        sums, rng_, steps = D.run_protocol(world, rank, len(pts), myW, 3, solve_range, ar, ag)
+        res = ("ok", sums, rng_, steps)
+    except RuntimeError as e:
+        res = (type(e).__name__, str(e), None, None)
+    except ValueError as e:
+        res = ("ValueError", str(e), None, None)
+    out_q.put((rank, res))
+    dist.barrier()          # every rank got here: nobody hangs in a collective
+    dist.destroy_process_group()
+
+
+def _run_protocol_world(world, W, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_protocol_worker, args=(r, world, port, W, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_library_protocol_over_gloo_with_oracle_shards(world):
+    """wost_distributed_run over gloo: rank r's walk range of every point comes from
+    the CPU oracle (the device's Philox streams), the C++ agreement all-reduce,
+    padded all-gather and ordered merge give one rank's sums bit for bit on every
+    rank, and total_steps counts every rank's walk-steps."""
+    from dcrmontecarlo_amd import scenarios as S
+
+    W = 3 * 4096 + 1000
+    res = _run_protocol_world(world, W, "ok")
+    sc = S.poisson_square()
+    single = D.merge_walk_range_blocks([_oracle_range_blocks(sc, sc.points[:3], W, 0, W, 99)], W)
+    for r in range(world):
+        status, sums, (w0, w1), steps = res[r]
+        assert status == "ok"
+        assert np.array_equal(sums, single)
+        assert (w0, w1) == D.shard_walk_range(W, world, r)
+        assert steps == int(single[:, 2].sum())
+
+
+def test_library_protocol_failure_on_one_rank_reaches_every_rank():
+    """a rank whose local solve fails still takes part in the agreement
+    collective, so every rank returns an error instead of waiting in the gather:
+    the failing rank re-raises its own exception, the others get WostError."""
+    res = _run_protocol_world(2, 2 * 4096, "fail")
+    assert res[1][0] == "RuntimeError" and "injected failure" in res[1][1]
+    assert res[0][0] == "WostError" and "another rank failed" in res[0][1]
+
+
+def test_library_protocol_rejects_disagreeing_ranks():
+    """Ranks called with different walk counts agree to fail (ValueError on all)."""
+    res = _run_protocol_world(2, 2 * 4096, "disagree")
+    for r in range(2):
+        assert res[r][0] == "ValueError" and "disagree" in res[r][1], res[r]
+
+
+def test_library_protocol_eight_thread_ranks_with_oracle_shards():
+    """R = 8 (the driver's node size) through wost_distributed_run with thread ranks:
+    oracle walk shards of 3 points, ragged (W not a multiple of 8 blocks, some ranks
+    empty), one rank's sums on every rank."""
+    from dcrmontecarlo_amd import scenarios as S
+    from rank_threads import RankThreads
+
+    sc = S.poisson_square()
+    pts = sc.points[:3]
+    W = 5 * 4096 + 17                       # 6 blocks over 8 ranks: two ranks hold none
+    full = _oracle_range_blocks(sc, pts, W, 0, W, 5)
+    single = D.merge_walk_range_blocks([full], W)
+    R = 8
+
+    def shard(w0, w1):
+        return full[:, w0 // 4096:-(-w1 // 4096)]
+
+    res = RankThreads(R).run(lambda r, ar, ag: D.run_protocol(R, r, len(pts), W, 3, shard, ar, ag))
+    assert sum(1 for r in range(R) if res[r][1][0] == res[r][1][1]) == 2
+    for r in range(R):
+        assert np.array_equal(res[r][0], single)

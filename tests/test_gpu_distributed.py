@@ -2,8 +2,11 @@
 
 wost_solve_range must reproduce, block for block and bit for bit, the blocks of
 the full solve it is a shard of; wost_solve_distributed on a one-rank
-communicator must equal wost_solve bit for bit (the N > 1 merge is covered by
-the gloo tests in test_distributed.py: RCCL cannot put two ranks on one GPU).
+communicator must equal wost_solve bit for bit. RCCL cannot put two ranks on one
+GPU, so the R > 1 path of wost_solve_distributed -- its C++ protocol
+wost_distributed_run (agreement all-reduce, padded all-gather, ordered merge) --
+runs here with R threads as ranks on real device shards (R = 2, 3, 8; single- and
+multi-source rows), and over gloo with oracle shards in test_distributed.py.
 """
 import numpy as np
 import pytest
@@ -112,9 +115,11 @@ def test_solve_distributed_one_rank_equals_solve(gpu_available, name):
 
 def test_shards_of_a_solve_merge_to_the_solve(gpu_available):
     """What each rank of an R-rank wost_solve_distributed computes -- its walk range of every
-    point -- merged in rank order equals the one-GPU point sums bit for bit (R = 2, 3, 8),
-    run here one shard after another on one GPU."""
+    point, solved on the device -- goes through libwost's own protocol (wost_distributed_run,
+    R threads as ranks): the merged point sums equal the one-GPU sums bit for bit on every
+    rank (R = 2, 3, 8), with the host mirror agreeing."""
     from dcrmontecarlo_amd import distributed as D
+    from rank_threads import RankThreads
 
     sc, s = _solver("dcr_dipole")
     pts = sc.points[:6]
@@ -122,13 +127,52 @@ def test_shards_of_a_solve_merge_to_the_solve(gpu_available):
     sums = s.solve_blocks(pts, W, 0, s.num_blocks(len(pts), W), sc.max_steps, sc.eps, seed=3)
     one = D.point_sums(sums, len(pts))
     for R in (2, 3, 8):
-        parts = []
-        nb_max = -(-(-(-W // B)) // R)
-        for r in range(R):
+        shards = {}
+        for r in range(R):   # the device solves, one after another
             w0, w1 = D.shard_walk_range(W, R, r)
-            p = np.zeros((len(pts), nb_max, 3))
-            if w1 > w0:
-                blk = s.solve_range(pts, W, w0, w1, sc.max_steps, sc.eps, seed=3)
-                p[:, :blk.shape[1]] = blk
-            parts.append(p)
-        assert np.array_equal(D.merge_walk_range_blocks(parts, W), one), R
+            shards[(w0, w1)] = s.solve_range(pts, W, w0, w1, sc.max_steps, sc.eps, seed=3) if w1 > w0 else None
+        res = RankThreads(R).run(lambda r, ar, ag: D.run_protocol(R, r, len(pts), W, 3,
+                                                                  lambda w0, w1: shards[(w0, w1)], ar, ag))
+        for r in range(R):
+            assert not isinstance(res[r], Exception), res[r]
+            assert np.array_equal(res[r][0], one), R
+            assert res[r][1] == D.shard_walk_range(W, R, r)
+            assert res[r][2] == int(one[:, 2].sum())
+
+
+def test_multi_source_shards_merge_through_the_protocol(gpu_available):
+    """Multi-source rows (2S+1 = 7) through wost_distributed_run with R = 3 thread ranks:
+    equal to one-GPU solve_sources bit for bit; and comm.solve_sources_distributed on a
+    one-rank RCCL communicator equals solve_sources."""
+    from dcrmontecarlo_amd import comm
+    from dcrmontecarlo_amd import distributed as D
+    from rank_threads import RankThreads
+
+    sc, s = _solver("dcr_dipole")
+    pts = sc.points[10:14]
+    W = 4 * B + 77
+    srcs = [sc.f, 2.0 * sc.f, 0.5 * sc.f]
+    u1, st1 = s.solve_sources(pts, srcs, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=8, return_stats=True)
+    fields = s.source_fields(srcs)
+    R = 3
+    with s.sources_installed(fields):
+        shards = {D.shard_walk_range(W, R, r): s.solve_range(pts, W, *D.shard_walk_range(W, R, r), sc.max_steps,
+                                                              sc.eps, seed=8) for r in range(R)}
+    res = RankThreads(R).run(lambda r, ar, ag: D.run_protocol(R, r, len(pts), W, 7, lambda a, b: shards[(a, b)],
+                                                              ar, ag))
+    for r in range(R):
+        sums = res[r][0]
+        for k in range(3):
+            assert np.array_equal(sums[:, 2 * k] / W, st1.mean[k])
+    c = comm.Communicator(comm.unique_id(), 1, 0, 0)
+    try:
+        ud, std, t = comm.solve_sources_distributed(s, c, pts, srcs, W, sc.max_steps, sc.eps, seed=8)
+        assert np.array_equal(ud, u1) and np.array_equal(std.stderr, st1.stderr)
+        assert t["all_steps"] == st1.total_steps
+        with pytest.raises(ValueError):
+            with s.sources_installed(fields):
+                comm.solve_distributed(s, c, pts, W, sc.max_steps, sc.eps, seed=8)
+        with pytest.raises(ValueError):
+            c.allreduce([1.0], "min")
+    finally:
+        c.close()

@@ -148,3 +148,88 @@ def test_dipole_source_is_antisymmetric_and_normalised():
     h = x[1] - x[0]
     pos = np.where(X < 0, v, 0).sum() * h * h
     assert pos == pytest.approx(1.0, rel=1e-3)
+
+
+class _FakeSolver:
+    """solve_sources stand-in: u_k(x) = a k-dependent linear function of the point, so the
+    survey's group/transmitter bookkeeping can be checked on the host."""
+
+    sigma_bar = 10.0
+
+    def __init__(self, scale):
+        self.scale = scale
+        self.calls = []
+
+    def values(self, pts, srcs):
+        k = np.array([float(np.asarray(s(np.array([0.0, -50.0])))) for s in srcs])   # identifies the source
+        return self.scale * (k[:, None] * 1e3 + pts[:, 0][None, :])
+
+    def solve_sources(self, pts, srcs, nWalks, maxSteps, eps, seed, return_stats):
+        from dcrmontecarlo_amd.solvers.WoStSolver import SolveStats
+
+        self.calls.append((len(pts), len(srcs), seed))
+        u = self.values(np.asarray(pts), srcs)
+        st = SolveStats(mean=u, stderr=np.full_like(u, 1e-6), mean_steps=np.ones(len(pts)), walks=nWalks,
+                        total_steps=len(pts) * nWalks, kernel_ms=1.0, total_ms=1.0)
+        return u.astype(np.float32), st
+
+
+@pytest.mark.parametrize("E,a", [(40, 1), (23, 2)])
+def test_wenner_survey_bookkeeping_one_gpu_and_communicator(E, a, monkeypatch):
+    """run_wenner_survey on host stand-ins: every quadripole's dV is u_q(M) - u_q(N) of
+    its own transmitter, each group is solved once per field with its own seed, and the
+    communicator path (comm.solve_sources_distributed; one communicator or a pair) fills
+    the same tables and counts the ranks' walk-steps."""
+    from dcrmontecarlo_amd import comm as C
+
+    sc = S.wenner_topography(n_electrodes=E, n_walks=8, n_segments=100)
+    Q = E - 3 * a
+    srcs = [survey.dipole_source(sc.points[q], sc.points[q + 3 * a], 0.5) for q in range(Q)]
+    fm, fh = _FakeSolver(1.0), _FakeSolver(0.5)
+    r1 = survey.run_wenner_survey(sc, 1e-2, 8, a=a, seed=3, solvers=(fm, fh), concurrent=False)
+    groups = list(survey.wenner_batches(E, a))
+    assert len(fm.calls) == len(fh.calls) == len(groups) == r1.launches
+    assert len({c[2] for c in fm.calls}) == len(groups)            # a seed per group
+    assert [c[2] for c in fm.calls] == [c[2] for c in fh.calls]    # common random numbers
+    quad = survey.wenner_quadripoles(E, a)
+    for q, (A, M, N, B) in enumerate(quad):
+        u = fm.values(sc.points[[M, N]], [srcs[q]])[0]
+        assert r1.model.dv[q] == pytest.approx(u[0] - u[1], rel=1e-12)
+    np.testing.assert_allclose(r1.rho.rho_a, 1e2 * 2.0)
+    assert r1.walk_steps == r1.local_walk_steps == 2 * E * 8
+
+    def fake_dist(solver, comm, pts, sources, nWalks, maxSteps, eps, seed=0):
+        u, st = solver.solve_sources(pts, sources, nWalks, maxSteps, eps, seed, True)
+        st.total_steps *= comm.n_ranks
+        return u, st, {"total_steps": st.total_steps // comm.n_ranks}
+
+    monkeypatch.setattr(C, "solve_sources_distributed", fake_dist)
+
+    class _Comm:
+        n_ranks = 4
+
+    for comm in (_Comm(), (_Comm(), _Comm())):
+        fm.calls.clear()
+        r2 = survey.run_wenner_survey(sc, 1e-2, 8, a=a, seed=3, solvers=(fm, fh), comm=comm)
+        assert np.array_equal(r2.model.dv, r1.model.dv) and np.array_equal(r2.background.dv, r1.background.dv)
+        assert r2.walk_steps == 4 * r2.local_walk_steps == 4 * r1.walk_steps
+
+
+def test_apparent_resistivity_resolves_only_with_the_model_error_small():
+    """resolved needs the model's dV resolved too (round-2 verdict): a precise background
+    with a model dV inside its own noise is not a resolved rho_a."""
+    h = survey.DipoleData(np.array([1.0, 1.0]), np.array([1e-3, 1e-3]))
+    m = survey.DipoleData(np.array([0.5, 0.5]), np.array([0.01, 1.0]))
+    r = survey.apparent_resistivity(m, h, 100.0)
+    assert r.resolved.tolist() == [True, False]
+
+
+def test_physical_wenner_variant_drops_only_the_air_term():
+    lit = S.wenner_topography(n_electrodes=8, n_walks=1, n_segments=100)
+    phys = S.wenner_topography_physical(n_electrodes=8, n_walks=1, n_segments=100)
+    assert phys.name == "wenner_topography_physical" and np.array_equal(phys.points, lit.points)
+    below = np.array([[0.0, -300.0], [-120.0, -80.0], [120.0, -80.0]])
+    np.testing.assert_allclose(np.asarray(phys.alpha(below), np.float64), np.asarray(lit.alpha(below), np.float64),
+                               rtol=1e-6)
+    above = np.array([[0.0, 2.5]])          # under the topography crest, above y = 0
+    assert float(np.asarray(lit.alpha(above)).ravel()[0]) < 1e-6 < float(np.asarray(phys.alpha(above)).ravel()[0])

@@ -314,11 +314,17 @@ def gen_sampler_draws(n=20000):
 # ---------------------------------------------------------------------------
 # G5: replay the reference on the Philox stream
 # ---------------------------------------------------------------------------
-def replay(name, points, n_walks, max_steps, eps, seed):
-    spec = ref_scenarios()[name]()
+_NODES = {}
+
+
+def replay(name, points, n_walks, max_steps, eps, seed, wid0=0, spec=None, values_only=False):
+    """The reference's solve() on the Philox stream. Walk ids start at wid0 and count
+    up per walk (point-major), so a job holding walks [c0, c0+n) of point e of a
+    W-walk solve passes wid0 = e*W + c0 and replays exactly those walks."""
+    spec = spec if spec is not None else ref_scenarios()[name]()
     solver = build_ref_solver(spec)
     k0, k1 = seed & M32, (seed >> 32) & M32
-    st = {"wid": 0, "step": -1, "nrand": 0}
+    st = {"wid": wid0, "step": -1, "nrand": 0}
     cache = {}
 
     def draw():
@@ -347,7 +353,10 @@ def replay(name, points, n_walks, max_steps, eps, seed):
         return v
 
     solver.boundaryDirichlet = bc
-    nodes = screened_nodes(solver.sigma_bar) if solver.use_delta_tracking else greens_nodes()
+    nkey = float(solver.sigma_bar) if solver.use_delta_tracking else None
+    if nkey not in _NODES:
+        _NODES[nkey] = screened_nodes(solver.sigma_bar) if solver.use_delta_tracking else greens_nodes()
+    nodes = _NODES[nkey]
 
     class FakeSampler:
         def __init__(self, *a, **k):
@@ -376,6 +385,11 @@ def replay(name, points, n_walks, max_steps, eps, seed):
     finally:
         torch.rand = orig_rand
         ref_mod.GreensDistribution2D, ref_mod.ScreenedGreensDistribution2D = oG, oS
+    if values_only:
+        v = np.array([sum(float(c["contribution"]) for c in wk["contributions"]) for pi in range(len(points))
+                      for wk in hist[pi]], np.float64)
+        s = np.array([len(wk["path"]) for pi in range(len(points)) for wk in hist[pi]], np.int32)
+        return v, s, float(solver.sigma_bar)
     vals, steps, finals = [], [], []
     # the recorded histories themselves (golden vectors of the walk recorder)
     path_pts, path_dd, path_dn, src_pts, src_vals, bnd_vals, totals = [], [], [], [], [], [], []
@@ -553,12 +567,64 @@ def gen_rho(walks, workers, chunk=50):
     print("rho_dcr_dipole.npz", f"{time.time() - t0:.0f}s", "common paths", same, "sigma_bar", sbar)
 
 
+# ---------------------------------------------------------------------------
+# G9: the C4 survey replayed on the Philox stream -- every electrode's walks of the
+# reference for the model conductivity and the alpha = 100 background, so that its
+# dipole-dipole apparent resistivities are pinned walk for walk, independent of
+# Monte-Carlo error (WoStSolver.py:226,244,272 redirected as in G5)
+# ---------------------------------------------------------------------------
+RHO_REPLAY_SEED = 2024
+
+
+def _rho_replay_worker(args):
+    field, e, c0, n, W, ms, eps = args
+    torch.set_num_threads(1)
+    sc = S.dcr_dipole()
+    pt = np.ascontiguousarray(sc.points[e:e + 1], np.float32)
+    v, s, sb = replay("dcr_dipole", pt, n, ms, eps, RHO_REPLAY_SEED, wid0=e * W + c0, spec=_rho_spec(field),
+                      values_only=True)
+    return field, e, c0, v, s, sb
+
+
+def gen_rho_replay(walks, workers, chunk=100):
+    import multiprocessing as mp
+
+    sc = S.dcr_dipole()
+    pts = np.ascontiguousarray(sc.points, np.float32)
+    E = len(pts)
+    _NODES[10.0] = screened_nodes(10.0)     # both fields: sigma_bar = 10 (Q8 fallback); forked workers inherit
+    jobs = [(field, e, c0, min(chunk, walks - c0), walks, sc.max_steps, sc.eps)
+            for c0 in range(0, walks, chunk) for e in range(E) for field in ("model", "background")]
+    vals = {f: np.zeros((E, walks)) for f in ("model", "background")}
+    steps = {f: np.zeros((E, walks), np.int32) for f in ("model", "background")}
+    sbar = {}
+    t0 = time.time()
+    done = 0
+    with mp.get_context("fork").Pool(workers) as pool:
+        for field, e, c0, v, s, sb in pool.imap_unordered(_rho_replay_worker, jobs):
+            vals[field][e, c0:c0 + len(v)] = v
+            steps[field][e, c0:c0 + len(s)] = s
+            sbar[field] = sb
+            done += 1
+            if done % 48 == 0:
+                print(f"rho_replay: {done}/{len(jobs)} jobs, {time.time() - t0:.0f}s", flush=True)
+    same = bool(np.array_equal(steps["model"], steps["background"]))
+    np.savez_compressed(os.path.join(OUT, "rho_replay_dcr_dipole.npz"), points=pts, n_walks=np.int64(walks),
+                        max_steps=np.int64(sc.max_steps), eps=np.float32(sc.eps), alpha_bg=np.float64(RHO_ALPHA_BG),
+                        seed=np.uint64(RHO_REPLAY_SEED), model_values=vals["model"],
+                        background_values=vals["background"], model_steps=steps["model"],
+                        background_steps=steps["background"], sigma_bar_model=np.float64(sbar["model"]),
+                        sigma_bar_background=np.float64(sbar["background"]), common_paths=np.bool_(same))
+    print("rho_replay_dcr_dipole.npz", f"{time.time() - t0:.0f}s", "common paths", same, "sigma_bar", sbar)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="geometry,fields,greens,sampler,replay,stats")
     ap.add_argument("--scenarios", default="")
     ap.add_argument("--stats-workers", type=int, default=8)
     ap.add_argument("--rho-walks", type=int, default=400)
+    ap.add_argument("--rho-replay-walks", type=int, default=256)
     a = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     parts = set(a.only.split(","))
@@ -578,6 +644,8 @@ def main():
         gen_stats(names, a.stats_workers)
     if "rho" in parts:
         gen_rho(a.rho_walks, a.stats_workers)
+    if "rho_replay" in parts:
+        gen_rho_replay(a.rho_replay_walks, a.stats_workers)
 
 
 if __name__ == "__main__":
