@@ -54,9 +54,10 @@ def parse():
     ap.add_argument("--workload", choices=["dcr_dipole", "wenner_topography"], default="dcr_dipole")
     ap.add_argument("--walks", type=int, default=None,
                     help="walks per electrode per GPU (dcr_dipole 1M, wenner_topography 100k)")
-    ap.add_argument("--literal", action="store_true",
-                    help="wenner_topography: the notebook's conductivity with its air term (default: the "
-                         "physical variant without it, so rho_a is meaningful)")
+    ap.add_argument("--fields", choices=["literal", "physical"], default="literal",
+                    help="wenner_topography: the notebook's conductivity with its air term (literal, SURVEY 8d "
+                         "C5; the timed survey) or without it (physical); the rho_a report always comes from "
+                         "a physical survey")
     ap.add_argument("--no-bruteforce", action="store_true", help="wenner_topography: skip the scan-kernel leg")
     ap.add_argument("--electrodes", type=int, default=None, help="dcr_dipole 48, wenner_topography 256")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
@@ -336,6 +337,8 @@ def main():
         fps = perfmodel.flops_per_step(sc)
         # dominant kernel: the walk kernel on this rank (HIP events on libwost's stream)
         ach_tflops = fps * steps_local / (kernel_ms * 1e-3) / 1e12
+        fps_exec = perfmodel.executed_flops_per_step(sc)
+        exec_tflops = fps_exec * steps_local / (kernel_ms * 1e-3) / 1e12
         bytes_per_launch = perfmodel.hbm_bytes_per_walk() * (len(sc.points) * (w1 - w0))
         ach_gbs = bytes_per_launch * launches / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
         mean = last_sums[:, 0] / Wt
@@ -365,6 +368,10 @@ def main():
                          # (profiles/traffic_dcr_dipole.json) vs the algorithmic 8 B per walk
                          "traffic": measured_traffic(), "algorithmic_bytes_per_launch": bytes_per_launch,
                          "model_flops_per_step": fps, "flop_model": "SURVEY.md 8(d) v1 per-config total (C4 ~350)",
+                         # the same model without the ~120 FLOP i0e series the kernel replaced by
+                         # an LDS table lookup: the FP32 work it executes
+                         "executed_flops_per_step": fps_exec, "achieved_executed": exec_tflops,
+                         "frac_executed": exec_tflops / perfmodel.FP32_PEAK_TFLOPS,
                          "kernel": "wost_walk_jit (hiprtc field-specialised, mixed+delta)" if jit
                          else "wost_walk_kernel<true,true,true> (precompiled)",
                          "kernel_ms_per_launch": kernel_ms / max(launches, 1),
@@ -449,7 +456,7 @@ def wenner_main(args, world, rank, local):
 
     W1 = args.walks or 100_000
     E = args.electrodes or 256
-    sc = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=not args.literal)
+    sc = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=args.fields == "physical")
     sm = sc.solver(device=local)
     sh = survey.homogeneous_solver(sc, WENNER_ALPHA_BG, sm, device=local)
     comms = None
@@ -480,6 +487,12 @@ def wenner_main(args, world, rank, local):
     barrier()
     elapsed = time.perf_counter() - t0
     max_elapsed = elapsed if comms is None else float(comms[0].allreduce([elapsed], "max")[0])
+    res_phys = None
+    if args.fields == "literal":   # outside the timed region: the physical survey's rho_a
+        sp = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=True)
+        pm = sp.solver(device=local)
+        ph = survey.homogeneous_solver(sp, WENNER_ALPHA_BG, pm, device=local)
+        res_phys = survey.run_wenner_survey(sp, WENNER_ALPHA_BG, Wt, seed=4242, solvers=(pm, ph), comm=comms)
 
     if rank == 0:
         value = steps_all / max_elapsed
@@ -531,12 +544,22 @@ def wenner_main(args, world, rank, local):
                 "bruteforce_frac_fp32": rate_bf * bs / 1e12 / perfmodel.FP32_PEAK_TFLOPS}
         out["cpu_baseline"] = (wenner_cpu_leg(sc, sm.sigma_bar or 0.0, args.cpu_seconds)
                                if (not args.no_cpu and world == 1) else None)
-        out["rho_a"] = {"array": f"Wenner-alpha a = 1, {len(res.quadripoles)} quadripoles", "rho_bg": 1 / WENNER_ALPHA_BG,
-                        "resolved": int(ok.sum()),
-                        "median": float(np.median(res.rho.rho_a[ok])) if ok.any() else None,
-                        "p10_p90": [float(np.percentile(res.rho.rho_a[ok], q)) for q in (10, 90)] if ok.any() else None,
-                        "mc_1sigma_rms": float(np.sqrt(np.mean(res.rho.se[ok] ** 2))) if ok.any() else None,
-                        "rho_a_checksum": float(np.sum(res.rho.rho_a[ok]))}
+        def rho_summary(r, what):
+            good = r.rho.resolved & np.isfinite(r.rho.rho_a)
+            return {"survey": what, "array": f"Wenner-alpha a = 1, {len(r.quadripoles)} quadripoles",
+                    "rho_bg": 1 / WENNER_ALPHA_BG, "resolved": int(good.sum()),
+                    "median": float(np.median(r.rho.rho_a[good])) if good.any() else None,
+                    "p10_p90": [float(np.percentile(r.rho.rho_a[good], q)) for q in (10, 90)] if good.any() else None,
+                    "mc_1sigma_rms": float(np.sqrt(np.mean(r.rho.se[good] ** 2))) if good.any() else None,
+                    "rho_a_checksum": float(np.sum(r.rho.rho_a[good]))}
+
+        if args.fields == "physical":
+            out["rho_a"] = rho_summary(res, f"the timed survey ({sc.name})")
+        else:
+            out["rho_a"] = rho_summary(res_phys, f"wenner_topography_physical, {Wt} walks per electrode, untimed "
+                                                 "(the literal fields put the electrodes in 'air': "
+                                                 "their rho_a is not physical)")
+            out["rho_a_literal_timed_survey"] = rho_summary(res, sc.name)
         print(json.dumps(out), flush=True)
     if comms is not None:
         comms[0].barrier()

@@ -378,30 +378,11 @@ float silhouette_stop2(float rmin) {
     return x;
 }
 
-// LDS staging of the segment tree's top levels (wost_walk.h, SegTree::lds): with
-// WOST_TREE_LDS=<records> (> 0) the field-specialised tree kernels run 896-thread
-// workgroups, two per CU (7 waves per SIMD, as the register budget allows), each
-// staging up to <records> records (whole levels, at most half the CU's 160 KiB of
-// LDS). Off by default: on C5 it measured slower than reading the records through
-// L1/L2 with 256-thread workgroups (4.09e9 with 511 records, 3.94e9 with 127, vs
-// 4.74e9 walk-steps/s; profiles/r02_tree/ab_tree_lds.log) -- the top levels stay
-// L1-resident anyway and the generic (flat) loads that serve both address spaces
-// cost more than the global ones.
-constexpr int kTreeBlock = 896;
-constexpr size_t kTreeLdsBudget = 80 * 1024;
-
-int tree_lds_records(const wost_handle* h, int mode, int n_points, int* block) {
+// The segment tree's records are read through L1/L2 by 256-thread workgroups (LDS
+// staging of its top levels measured slower in round 2: profiles/r02_tree/ab_tree_lds.log).
+int tree_lds_records(const wost_handle*, int, int, int* block) {
     *block = kWalkBlock;
-    const char* e = std::getenv("WOST_TREE_LDS");
-    if (!mode_tree(mode) || !e) return 0;
-    const int nd = (int)(h->dverts.size() / 2), nn = (int)(h->nverts.size() / 2);
-    const size_t base = walk_lds_bytes(mode, nd, nn, n_points, 0);
-    int n = base < kTreeLdsBudget ? (int)((kTreeLdsBudget - base) / (4 * sizeof(float4))) : 0;
-    n = std::min(std::min(n, h->tree.first_leaf), std::max(0, std::atoi(e)));
-    int full = 0;                      // whole levels only
-    while (2 * full + 1 <= n) full = 2 * full + 1;
-    if (full > 0) *block = kTreeBlock;
-    return full;
+    return 0;
 }
 
 bool use_tree(const wost_handle* h) {
@@ -859,6 +840,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_tol = h->tree.tol;
         a.tree_stop2 = silhouette_stop2(a.rmin);
         a.tree_lds_records = tree_lds;
+        a.tree_depth = h->tree.depth;
     }
 
     if (mode_delta(mode) && n_points > 0) {   // alpha at the query points, with the walk kernel's fields

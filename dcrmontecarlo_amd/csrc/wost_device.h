@@ -1113,71 +1113,147 @@ WOST_HD Hit intersect_polylines_compact(VP v, SP sv, float px, float py, float d
     return intersect_finish<false>(v, bi, best, px, py, dx, dy, qx, qy, r);
 }
 
+// intersect_polylines over compiled-in vertices v (NV <= 65), two passes with a
+// cheaper candidate filter than intersect_polylines_compact's: one signed line
+// distance per VERTEX, c_i = cross(d, v_i - q) (shared by the two segments at v_i),
+// and a segment is a candidate when its endpoints' c straddle the ray's line within
+// S. Every segment the exact test accepts has a point within 2^-21.9 (|u|_1 +
+// |q - a|_1) of the line (the rounding of ns and den, see the tree's line test), and
+// c_i errs by at most 2^-21 (|v_i|_1 + |q|_1), so S = 2^-17 (c1 + |q|_1) with c1 =
+// max_i |v_i|_1 (a literal of the generated kernel) keeps a strict superset with a
+// 4x margin. No reciprocal per segment; crossings behind q stay candidates, which
+// the exact test (the same function on the staged copy sv, ascending, so `s < best`
+// keeps the first argmin) then rejects. Bit for bit intersect_polylines.
+template <int NV, class VP, class SP>
+WOST_HD Hit intersect_polylines_lines(VP v, SP sv, float px, float py, float dxi, float dyi, float r, float c1) {
+#pragma clang fp contract(off)
+    static_assert(NV >= 2 && NV <= 65, "one bit per segment");
+    Hit h;
+    float dn, dx, dy;
+    unit_direction(dxi, dyi, dn, dx, dy);
+    if (dn < 1e-10f) {
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
+        return h;
+    }
+    const float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
+    const float m = fmaf(dx, qy, -(dy * qx));                              // cross(d, q)
+    const float S = 7.62939453125e-06f * (c1 + (fabsf(qx) + fabsf(qy)));   // 2^-17
+    uint64_t cand = 0ull;
+    float cprev = fmaf(dx, v[0].y, -(dy * v[0].x)) - m;
+#pragma unroll
+    for (int i = 1; i < NV; ++i) {
+        const float c = fmaf(dx, v[i].y, -(dy * v[i].x)) - m;              // cross(d, v_i - q) within its bound
+        if (fminf(cprev, c) <= S && fmaxf(cprev, c) >= -S) cand |= 1ull << (i - 1);
+        cprev = c;
+    }
+    float best = WOST_INF;
+    int bi = -1;
+    while (cand != 0ull) {
+        const int j = __builtin_ctzll(cand);
+        cand &= cand - 1ull;
+        const float s = ray_segment_time_filtered(sv[j], sv[j + 1], qx, qy, dx, dy);
+        if (s < best) { best = s; bi = j; }
+    }
+    return intersect_finish<false>(v, bi, best, px, py, dx, dy, qx, qy, r);
+}
+
+// silhouette_distance over compiled-in vertices v (NV <= 65) in two passes: the
+// unrolled scan forms each segment's cross product once (as silhouette_distance,
+// the same operands and rounding) and marks the silhouette vertices in a bit mask;
+// then each lane takes the squared distances of its own silhouette vertices only,
+// from the staged copy sv (x - b and its squares as silhouette_distance forms them).
+// The minimum does not depend on the order: bit for bit silhouette_distance.
+template <int NV, class VP, class SP>
+WOST_HD float silhouette_distance_compact(VP v, SP sv, float px, float py) {
+#pragma clang fp contract(off)
+    static_assert(NV >= 3 && NV <= 66, "one bit per interior vertex");
+    uint64_t sil = 0ull;
+    float cprev = (v[1].x - v[0].x) * (py - v[0].y) - (v[1].y - v[0].y) * (px - v[0].x);
+#pragma unroll
+    for (int j = 1; j + 1 < NV; ++j) {
+        const float bpx = px - v[j].x, bpy = py - v[j].y;
+        const float ccur = (v[j + 1].x - v[j].x) * bpy - (v[j + 1].y - v[j].y) * bpx;
+        if (cprev * ccur < 0.0f) sil |= 1ull << (j - 1);
+        cprev = ccur;
+    }
+    float best = WOST_INF;
+    while (sil != 0ull) {
+        const int j = __builtin_ctzll(sil) + 1;
+        sil &= sil - 1ull;
+        const float2 b = sv[j];
+        const float bpx = px - b.x, bpy = py - b.y;
+        const float d2 = bpx * bpx + bpy * bpy;
+        best = d2 < best ? d2 : best;
+    }
+    return best == WOST_INF ? best : sqrt_rn(best);
+}
+
 // ---------------------------------------------------------------------------
 // Segment tree over a long Neumann polyline (topography with 10^4+ segments).
 // The reference scans every segment at every step (PolylinesSimple.py:83-102,
 // :134-197); these queries return the same bits while visiting only the parts
 // of the polyline that can matter.
 //
-// Implicit complete binary tree (built by wost_tree.cpp, build_segment_tree):
-// node k has children 2k+1 and 2k+2; leaves are nodes first_leaf.. and leaf l
-// owns segments [l*L, min((l+1)*L, nseg)). A node's range of segments also
-// includes the first segment of its right neighbour (a vertex's silhouette
-// test reads both adjacent segments). A node is described by its bounding box
-// (xmin, ymin, xmax, ymax) of the range's vertices, exact (min/max of vertex
-// coordinates), and the arc of its segment directions as its two edge unit
-// vectors (e1, e2), see cone_excludes_silhouettes. Padding leaves have
-// inverted boxes.
+// Implicit complete 4-ary tree (built by wost_tree.cpp, build_segment_tree):
+// node k has children 4k+1 .. 4k+4; level d holds nodes (4^d-1)/3 ..; the
+// leaves are level `depth` and leaf l owns segments [l*L, min((l+1)*L, nseg)).
+// A node's range of segments also includes the first segment of its right
+// neighbour (a vertex's silhouette test reads both adjacent segments).
+// A node is described by an ORIENTED box -- centre c, unit axis u along the
+// node's mean segment direction, half-length a along u, half-width b across it
+// -- holding every vertex of its range (inflated on the host far beyond the
+// rounding of the stored values and of the kernels' corner arithmetic), and by
+// the half-angle h of the arc of its segment directions around u (cone codes:
+// cos h = 2 only zero-length segments, 3 directions too spread; a < 0 padding).
+// Along a gently sloping surface an oriented box is much thinner than an
+// axis-aligned one, so both queries prune far closer to the query point.
 //
-// Layout (BVH2 child records): internal node k stores its two CHILDREN's
-// descriptions in one 64-byte record rec[4k .. 4k+3] = {box(2k+1),
-// box(2k+2), cone(2k+1), cone(2k+2)}, so one step of a traversal tests both
-// children with four independent loads (one memory round trip per level).
-// The first `n_lds` records may be staged in LDS (TREE kernels: `lds`), the
-// rest are read from global memory. Traversals keep no stack: a bit per level
-// records a pending second child (and, for the nearest-first silhouette
-// search, which child it is); the ancestor at depth p of node k at depth d is
-// ((k + 1) >> (d - p)) - 1.
+// Layout (4-wide child records): internal node k stores its four CHILDREN's
+// descriptions in 8 float4s rec[8k .. 8k+7] = {c, u}, {a, b, cos h, sin h} per
+// child, read with global loads (the records stay L1/L2-resident). A traversal
+// keeps no stack: 4 bits per level mark the children of that level's node still
+// to visit; the ancestor at level p of the node at level d, position pos, is
+// position pos >> 2(d-p).
 //
-// Exactness:
-//  * the ray query prunes nodes whose box is farther than tol from the ray's
-//    LINE (behind or ahead); a segment the float test accepts lies within a few
-//    ulps of the line (tol is ~2^-14 of the coordinates, 10^3 times that), and
-//    leaves are visited in ascending segment order (left child first), so
-//    `s < best` keeps the first argmin like the scan;
-//  * the silhouette query prunes by a box lower bound on the squared distance,
-//    which rounds monotonically (contraction off) to at most any vertex's
-//    computed distance, and by the direction cone: when every segment
-//    direction of the node makes an angle of more than ~1e-3 rad with every
-//    view vector, all cross products c1, c2 of :63-81 have one sign and no
-//    vertex of the node is a silhouette. Vertices farther than the Dirichlet distance dd
-//    (+0.2%) cannot change min(dn, dd) (:212), so they are pruned too and the
-//    result is exact for that use. The visiting order (nearer lower bound
-//    first) only decides how soon `best` tightens the bound.
+// Exactness (the results are independent of the visiting order):
+//  * the ray query keeps the lexicographic minimum of (s, segment index) over
+//    the segments its float test accepts -- the scan's first argmin of s -- and
+//    prunes a node only when its box is farther than tol from the ray's LINE;
+//    every accepted segment has a point within 2^-22 (|u|_1 + |q - a|_1) of the
+//    line (the rounding of s = ns/den, ns and den), and tol is 2^-17 of the
+//    coordinates plus |q|_1, several times that plus the test's own rounding;
+//  * the silhouette query returns the minimum squared distance of the silhouette
+//    vertices it finds, pruning a node by a lower bound on the computed squared
+//    distance of every vertex in its box (with a slack above the rounding of the
+//    bound) and by the direction cone: when every segment direction of the node
+//    makes an angle of more than ~1e-5 rad with every view vector, all cross
+//    products c1, c2 of :63-81 have one sign and no vertex of the node is a
+//    silhouette. Vertices farther than the Dirichlet distance dd (+0.2%) cannot
+//    change min(dn, dd) (:212), so they are pruned too and the result is exact
+//    for that use. The nearer-first order only decides how soon the bound tightens.
 // ---------------------------------------------------------------------------
 struct SegTree {
-    const float4* rec;    // [4 * first_leaf] child records (global memory)
-    const float4* lds;    // the first n_lds records staged in LDS (or null)
-    int n_lds;
+    const float4* rec;    // [8 * first_leaf] child records (global memory)
     const float2* v;      // polyline vertices
     int nv;               // vertex count
-    int first_leaf;       // index of the first leaf node (= number of internal nodes)
+    int first_leaf;       // index of the first leaf node = number of internal nodes
+    int depth;            // level of the leaves
     int leaf;             // segments per leaf
     float tol;            // line-test tolerance at the origin; grows with |q|
-    WOST_HD const float4* record(int k) const { return k < n_lds ? lds + 4 * k : rec + 4 * k; }
-    // word i of record k. Kernels that stage no records (all but the WOST_TREE_LDS
-    // variants, wost_jit.cpp) read them with global loads: a pointer that may point to
-    // LDS or global memory compiles to generic (flat) loads, which cost more.
+    // word i (0..7) of internal node k's record, with a global load
     WOST_HD float4 word(int k, int i) const {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(WOST_TREE_LDS_KERNEL)
-        return ((const __attribute__((address_space(1))) float4*)rec)[4 * k + i];
+#if defined(__HIP_DEVICE_COMPILE__)
+        return ((const __attribute__((address_space(1))) float4*)rec)[8 * k + i];
 #else
-        return record(k)[i];
+        return rec[8 * k + i];
 #endif
     }
 };
 
-constexpr float kConeMargin = 1e-3f;
+#ifndef WOST_CONE_MARGIN
+#define WOST_CONE_MARGIN 1e-5f
+#endif
+constexpr float kConeMargin = WOST_CONE_MARGIN;
 
 #if defined(WOST_TREE_STATS) && !defined(__HIP_DEVICE_COMPILE__)
 extern long g_tree_stats[4];   // host harness only: silhouette records, leaves; ray records, leaves
@@ -1194,46 +1270,64 @@ WOST_HD int highest_bit(uint32_t m) {   // m != 0
 #endif
 }
 
-// True when no vertex of the node can be a silhouette seen from p. The cone
-// holds the two edge directions e1, e2 of the arc of the node's segment
-// directions (half-angle < pi/2). For segment u_i from a_i (both in the node),
-// c_i = cross(u_i, p - a_i) of :63-81. Over u in the arc, cross(u, w) is a
-// sinusoid whose minimum magnitude is at an edge; over a_i in the box it is
-// linear in p - a_i, extreme at a corner. So when the 8 values cross(e, p - q)
-// (e = e1, e2; q = box corners) share one sign with margin, every c_i has that
-// sign, c1 * c2 > 0 at every vertex, and none is a silhouette. The margin
-// (1e-3 of |p - q|_1) keeps every c_i far from the float rounding of its
-// evaluation. Codes: e1.x == 2: only zero-length segments (c == 0, never a
-// silhouette); e1.x == 3: directions too spread to prune.
-WOST_HD bool cone_excludes_silhouettes(float4 box, float4 cone, float px, float py) {
-#pragma clang fp contract(off)
-    if (cone.x == 2.0f) return true;
-    if (cone.x == 3.0f) return false;
-    const float wx0 = px - box.x, wx1 = px - box.z;
-    const float wy0 = py - box.y, wy1 = py - box.w;
-    const float mx = fmaxf(fabsf(wx0), fabsf(wx1)), my = fmaxf(fabsf(wy0), fabsf(wy1));
-    const float m = kConeMargin * (mx + my);
-    // cross(e, w) = e.x w.y - e.y w.x at the four corners, for both edges
-    const float a0 = cone.x * wy0, a1 = cone.x * wy1, b0 = cone.y * wx0, b1 = cone.y * wx1;
-    const float c0 = cone.z * wy0, c1 = cone.z * wy1, d0 = cone.w * wx0, d1 = cone.w * wx1;
-    const float v0 = a0 - b0, v1 = a0 - b1, v2 = a1 - b0, v3 = a1 - b1;
-    const float v4 = c0 - d0, v5 = c0 - d1, v6 = c1 - d0, v7 = c1 - d1;
-    const float lo = fminf(fminf(fminf(v0, v1), fminf(v2, v3)), fminf(fminf(v4, v5), fminf(v6, v7)));
-    const float hi = fmaxf(fmaxf(fmaxf(v0, v1), fmaxf(v2, v3)), fmaxf(fmaxf(v4, v5), fmaxf(v6, v7)));
-    return lo > m || hi < -m;
+WOST_HD int lowest_bit(uint32_t m) {    // m != 0
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ffs((int)m) - 1;
+#else
+    return __builtin_ctz(m);
+#endif
 }
 
-// Squared distance from p to the box (a lower bound of every vertex's computed
-// squared distance), +inf for an inverted (padding) box.
-WOST_HD float box_lower_bound2(float4 b, float px, float py) {
+// first node index of level d: (4^d - 1) / 3
+WOST_HD int tree_level_offset(int d) { return (int)(((1u << (2 * d)) - 1u) / 3u); }
+
+// Both pruning tests of a child in the box's own frame: w = p - c, pu = u . w (along
+// the axis), pn = cross(u, w) (across it).
+//
+// Lower bound of every vertex's computed squared distance from p: the distance to
+// the oriented box, less a slack above its rounding (+inf for padding).
+//
+// Silhouettes: for segment u_i from a_i (both in the node), c_i = cross(u_i, p - a_i)
+// of :63-81. Over directions e in the arc [u rotated by -h, +h], cross(e, w') is a
+// sinusoid in the angle, concave where positive (negative), so its extremes over
+// the arc are at the edges; over a_i in the box it is affine, extreme at a corner
+// q = c -+ a u -+ b n. With e1,2 = u rotated by -+h, cross(e1,2, p - q) =
+// cos h pn +- sin h pu -+ a sin h -+ b cos h, so every c_i has one sign -- c1 c2 >
+// 0 at every vertex, no silhouette -- when cos h |pn| - sin h |pu| > K = a sin h +
+// b cos h, with a margin of 1e-5 |p - q|_1, some 20 times the rounding of these
+// values and of any c_i. (The same bound the eight corner cross products give, in
+// six operations.)
+struct ChildFrame {
+    float wx, wy, pu, pn;
+};
+
+WOST_HD ChildFrame child_frame(float4 cu, float px, float py) {
 #pragma clang fp contract(off)
-    const float gx = fmaxf(fmaxf(b.x - px, px - b.z), 0.0f);
-    const float gy = fmaxf(fmaxf(b.y - py, py - b.w), 0.0f);
-    return b.x > b.z ? WOST_INF : gx * gx + gy * gy;
+    ChildFrame f;
+    f.wx = px - cu.x;
+    f.wy = py - cu.y;
+    f.pu = f.wx * cu.z + f.wy * cu.w;
+    f.pn = f.wy * cu.z - f.wx * cu.w;
+    return f;
 }
 
-WOST_HD bool silhouette_keep(float4 box, float4 cone, float lb, float bound, float px, float py) {
-    return !(lb > bound) && !cone_excludes_silhouettes(box, cone, px, py);
+WOST_HD float box_lower_bound2(float4 ab, const ChildFrame& f) {
+#pragma clang fp contract(off)
+    if (ab.x < 0.0f) return WOST_INF;
+    const float sl = 9.5367431640625e-07f * ((fabsf(f.wx) + fabsf(f.wy)) + (ab.x + ab.y));   // 2^-20
+    float gu = (fabsf(f.pu) - ab.x) - sl, gn = (fabsf(f.pn) - ab.y) - sl;
+    gu = gu > 0.0f ? gu : 0.0f;
+    gn = gn > 0.0f ? gn : 0.0f;
+    return (gu * gu + gn * gn) * 0.99999904632568359375f;   // 1 - 2^-20
+}
+
+WOST_HD bool cone_excludes_silhouettes(float4 ab, const ChildFrame& f) {
+#pragma clang fp contract(off)
+    if (ab.z == 2.0f) return true;
+    if (ab.z == 3.0f) return false;
+    const float K = (ab.x * ab.w + ab.y * ab.z) * 1.00000095367431640625f;   // a sin h + b cos h, rounded up
+    const float m = kConeMargin * ((fabsf(f.wx) + fabsf(f.wy)) + (ab.x + ab.y) * 2.0f);
+    return ab.z * fabsf(f.pn) - ab.w * fabsf(f.pu) > m + K;
 }
 
 // silhouette_distance for the use r = max(rmin, min(dn, dd)) of :210-212: exact
@@ -1248,21 +1342,46 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     const int nv = t.nv, nseg = nv - 1;
     if (nv < 3) return best;
     const float T = (dd * dd) * 1.002f;
-    int k = 0, depth = 0;
-    uint32_t pend = 0u, far_right = 0u;   // per level: second child pending / it is the right one
-    // resume the deepest pending second child, re-tested against the tightened bound;
+    int d = 0, pos = 0;     // the current node: level d, position pos in its level
+    uint32_t pend = 0u;     // 4 bits per level: children of that level's node still to visit
+    // test the children `cand` of node (lvl, at) against the bound: the kept ones,
+    // and the nearest of them in `nj`
+    auto visit = [&](int lvl, int at, uint32_t cand, int& nj) {
+        const int k = tree_level_offset(lvl) + at;
+        const float bound = best < T ? best : T;
+        uint32_t kept = 0u;
+        float nb = WOST_INF;
+        nj = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!((cand >> j) & 1u)) continue;
+            WOST_TREE_COUNT(0);
+            const float4 cu = t.word(k, 2 * j), ab = t.word(k, 2 * j + 1);
+            const ChildFrame f = child_frame(cu, px, py);
+            const float lb = box_lower_bound2(ab, f);
+            if (!(lb > bound) && !cone_excludes_silhouettes(ab, f)) {
+                kept |= 1u << j;
+                if (lb < nb) { nb = lb; nj = j; }
+            }
+        }
+        return kept;
+    };
+    // resume the deepest pending children, re-tested against the tightened bound;
     // false when nothing is pending (the search is over)
     auto resume = [&]() {
         while (pend != 0u) {
-            const int p = highest_bit(pend);
-            pend &= ~(1u << p);
-            const int anc = ((k + 1) >> (depth - p)) - 1;
-            const int side = (int)((far_right >> p) & 1u);
-            const float4 b = t.word(anc, side), c = t.word(anc, 2 + side);
-            const float bound = best < T ? best : T;
-            k = 2 * anc + 1 + side;
-            depth = p + 1;
-            if (silhouette_keep(b, c, box_lower_bound2(b, px, py), bound, px, py)) return true;
+            const int p = highest_bit(pend) >> 2;
+            const uint32_t m = (pend >> (4 * p)) & 15u;
+            pend &= ~(15u << (4 * p));
+            const int anc = pos >> (2 * (d - p));
+            int nj;
+            const uint32_t kept = visit(p, anc, m, nj);
+            if (kept) {
+                pend |= (kept & ~(1u << nj)) << (4 * p);
+                pos = 4 * anc + nj;
+                d = p + 1;
+                return true;
+            }
         }
         return false;
     };
@@ -1270,29 +1389,20 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     // other lanes have also left the internal nodes, then the leaves are scanned together
     bool live = true;
     while (live) {
-        while (live && k < t.first_leaf) {
-            WOST_TREE_COUNT(0);
-            const float4 bl = t.word(k, 0), br = t.word(k, 1), cl = t.word(k, 2), cr = t.word(k, 3);
-            const float bound = best < T ? best : T;
-            const float lbl = box_lower_bound2(bl, px, py), lbr = box_lower_bound2(br, px, py);
-            const bool okl = silhouette_keep(bl, cl, lbl, bound, px, py);
-            const bool okr = silhouette_keep(br, cr, lbr, bound, px, py);
-            if (okl || okr) {
-                const bool near_right = okr && (!okl || lbr < lbl);
-                const uint32_t bit = 1u << depth;
-                if (okl && okr) {
-                    pend |= bit;
-                    far_right = near_right ? (far_right & ~bit) : (far_right | bit);
-                }
-                k = 2 * k + 1 + (near_right ? 1 : 0);
-                ++depth;
+        while (live && d < t.depth) {
+            int nj;
+            const uint32_t kept = visit(d, pos, 15u, nj);
+            if (kept) {
+                pend |= (kept & ~(1u << nj)) << (4 * d);
+                pos = 4 * pos + nj;
+                ++d;
             } else {
                 live = resume();
             }
         }
         if (!live) break;
         WOST_TREE_COUNT(1);
-        const int s0 = (k - t.first_leaf) * t.leaf;
+        const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
         const int j1 = s1 < nv - 2 ? s1 : nv - 2;
         if (s0 + 1 <= j1) {
@@ -1319,11 +1429,12 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     return best == WOST_INF ? best : sqrt_rn(best);
 }
 
-// intersect_polylines over the tree: the same winner as the full scan.
-// NEAREST (compat="fixed"): intersect_polylines_ray's nearest crossing instead --
-// the same line pruning (every segment that test accepts lies on the ray's line
-// within tol as well), the same per-segment test, and leaves in ascending segment
-// order, so the strict t < best keeps the scan's first argmin; the same bits.
+// intersect_polylines over the tree: the same winner as the full scan -- the
+// lexicographic minimum of (s, segment) over the accepted segments.
+// NEAREST (compat="fixed"): intersect_polylines_ray's nearest crossing instead,
+// the lexicographic minimum of (t, segment) -- the same line pruning (every
+// segment that test accepts lies on the ray's line within tol as well) and the
+// same per-segment test; the same bits.
 template <bool NORMAL = true, bool NEAREST = false>
 WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float dxi, float dyi, float r) {
 #pragma clang fp contract(off)
@@ -1335,79 +1446,81 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
         return h;
     }
     const float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
-    const float tol = t.tol + 6.103515625e-05f * (fabsf(qx) + fabsf(qy));   // + 2^-14 |q|_1
+    const float tol = t.tol + 7.62939453125e-06f * (fabsf(qx) + fabsf(qy));   // + 2^-17 |q|_1
     const int nseg = t.nv - 1;
     float best = WOST_INF;
     int bi = -1;
-    // a box farther than tol from the ray's line holds no segment the float test accepts
-    auto line_keep = [&](float4 b) {
-        const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
-        const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
-        return !(b.x > b.z || fabsf(dx * cy - dy * cx) > fabsf(dx) * hy + fabsf(dy) * hx + tol);
+    // a box farther than tol from the ray's line holds no segment the float test
+    // accepts. A box wholly behind q holds none either when no segment direction of
+    // the node is within ~1e-3 rad of +-d: then |den| = |cross(d, u)| > 1e-3 |u| (|sin|
+    // over the arc is least at an edge), and a crossing behind by |t| >= 512 tol +
+    // 1e-2 L (L the box's L1 distance scale) has |nt| = |t| |den| >= 2^-8 |q| 1e-3 |u|
+    // + 1e-5 L |u|, some 30 times the rounding of nt (from q - a and the products),
+    // so the computed signs give t < 0 and the test fails. (Near-parallel segments
+    // can be accepted with flipped signs wherever they are, so such nodes are kept.)
+    auto keep = [&](float4 cu, float4 ab) {
+        if (ab.x < 0.0f) return false;
+        const float cx = cu.x - qx, cy = cu.y - qy;
+        const float cr = dx * cu.w - dy * cu.z, dt = dx * cu.z + dy * cu.w;   // cross(d, u), d . u
+        if (fabsf(dx * cy - dy * cx) > (ab.x * fabsf(cr) + ab.y * fabsf(dt)) + tol) return false;
+#if !defined(WOST_NO_TREE_BEHIND)
+        if (ab.z == 3.0f) return true;
+        const float ahead = (dx * cx + dy * cy) + (ab.x * fabsf(dt) + ab.y * fabsf(cr));   // max over the box of (x - q) . d
+        if (!(ahead < -(512.0f * tol + 1e-2f * ((fabsf(cx) + fabsf(cy)) + (ab.x + ab.y))))) return true;
+        if (ab.z == 2.0f) return false;
+        // cross(e1,2, d) = -(cos h cross(d, u)) +- sin h (d . u): both beyond 1e-3 with one
+        // sign iff cos h |cross(d, u)| - sin h |d . u| > 1e-3 (the edges' own rounding is
+        // ~1e-7, far inside that)
+        return !(ab.z * fabsf(cr) - ab.w * fabsf(dt) > 1e-3f);
+#else
+        return true;
+#endif
     };
-    // A box wholly behind q holds no segment the test accepts when no segment
-    // direction of the node is within ~1e-3 rad of +-d: then |den| = |cross(d, u)| >
-    // 1e-3 |u| (|sin| over the arc is least at an edge), and a crossing behind by
-    // |t| >= 64 tol + 1e-2 L (L the box's L1 distance scale) has |nt| = |t| |den| >=
-    // 2^-8 |q| 1e-3 |u| + 1e-5 L |u|, some 30 times the rounding of nt (from q - a
-    // and the products), so the computed signs give t < 0 and the test fails.
-    // (Near-parallel segments can be accepted with flipped signs wherever they are,
-    // so such nodes are kept.) Cone codes: 2 = only zero-length segments (never
-    // accepted), 3 = directions too spread to bound.
-    auto behind = [&](float4 b, float4 c) {
-        if (c.x == 3.0f) return false;
-        const float hx = 0.5f * (b.z - b.x), hy = 0.5f * (b.w - b.y);
-        const float cx = 0.5f * (b.x + b.z) - qx, cy = 0.5f * (b.y + b.w) - qy;
-        const float ahead = dx * cx + dy * cy + fabsf(dx) * hx + fabsf(dy) * hy;   // max over the box of (p - q) . d
-        if (!(ahead < -(64.0f * tol + 1e-2f * (fabsf(cx) + fabsf(cy) + hx + hy)))) return false;
-        if (c.x == 2.0f) return true;
-        const float c1 = c.x * dy - c.y * dx, c2 = c.z * dy - c.w * dx;              // cross(e1, d), cross(e2, d)
-        return (c1 > 1e-3f && c2 > 1e-3f) || (c1 < -1e-3f && c2 < -1e-3f);
-    };
-    int k = 0, depth = 0;
-    uint32_t pend = 0u;   // per level: the right child is pending
-    // the right child of the deepest pending level; false when nothing is pending
+    int d = 0, pos = 0;
+    uint32_t pend = 0u;   // 4 bits per level: children of that level's node still to visit
     auto resume = [&]() {
         if (pend == 0u) return false;
-        const int p = highest_bit(pend);
-        pend &= ~(1u << p);
-        k = 2 * (((k + 1) >> (depth - p)) - 1) + 2;
-        depth = p + 1;
+        const int p = highest_bit(pend) >> 2;
+        const int j = lowest_bit((pend >> (4 * p)) & 15u);
+        pend &= ~(1u << (4 * p + j));
+        pos = 4 * (pos >> (2 * (d - p))) + j;
+        d = p + 1;
         return true;
     };
     bool live = true;
     while (live) {                       // while-while, as in silhouette_distance_tree
-        while (live && k < t.first_leaf) {
+        while (live && d < t.depth) {
             WOST_TREE_COUNT(2);
-            const float4 b0 = t.word(k, 0), b1 = t.word(k, 1);
-#if defined(WOST_NO_TREE_BEHIND)
-            const bool okl = line_keep(b0), okr = line_keep(b1);
-#else
-            const bool okl = line_keep(b0) && !behind(b0, t.word(k, 2));
-            const bool okr = line_keep(b1) && !behind(b1, t.word(k, 3));
-#endif
-            if (okl || okr) {
-                if (okl && okr) pend |= 1u << depth;
-                k = 2 * k + (okl ? 1 : 2);   // left first: leaves in ascending segment order
-                ++depth;
+            const int k = tree_level_offset(d) + pos;
+            uint32_t kept = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (keep(t.word(k, 2 * j), t.word(k, 2 * j + 1))) kept |= 1u << j;
+            if (kept) {
+                const int j = lowest_bit(kept);
+                pend |= (kept & ~(1u << j)) << (4 * d);
+                pos = 4 * pos + j;
+                ++d;
             } else {
                 live = resume();
             }
         }
         if (!live) break;
         WOST_TREE_COUNT(3);
-        const int s0 = (k - t.first_leaf) * t.leaf;
+        const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
         if (s0 < s1) {
             float2 a = t.v[s0];
             for (int i = s0; i < s1; ++i) {
                 const float2 b = t.v[i + 1];
                 if (NEAREST) {
-                    const float tt = ray_segment_nearest_t(a, b, qx, qy, dx, dy, best);
-                    if (tt < best) { best = tt; bi = i; }
+                    // t <= best (ties too: the lower segment index wins them)
+                    const float bq = best < WOST_INF ? bits_to_float(__builtin_bit_cast(int32_t, best) + 1) : best;   // t > 0
+                    const float tt = ray_segment_nearest_t(a, b, qx, qy, dx, dy, bq);
+                    if (tt < best || (tt == best && i < bi)) { best = tt; bi = i; }
                 } else {
                     const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
-                    if (s < best) { best = s; bi = i; }
+                    if (s < best || (s == best && i < bi)) { best = s; bi = i; }
                 }
                 a = b;
             }

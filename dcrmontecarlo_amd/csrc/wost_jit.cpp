@@ -40,13 +40,15 @@ namespace {
 // whole-field saturation shortcut in the alpha jet (jet_body); 1024 compiled-in
 // Neumann ray scans unrolled by 2 instead of fully; 2048 sqrtf instead of
 // sqrt_rn for the distances; 4096 the tree's ray query
-// without its behind-the-origin pruning; 8192 the tree's records through generic
-// (flat) loads in kernels that stage none; 16384 the per-segment exact tests instead
-// of the two-pass scan (intersect_polylines_compact) for 8+ compiled-in segments.
+// without its behind-the-origin pruning; 8192 the per-segment reciprocal filter
+// (intersect_polylines_compact) instead of the per-vertex line filter
+// (intersect_polylines_lines); 16384 the per-segment exact tests instead of either
+// two-pass scan for 8+ compiled-in segments; 32768 the one-pass compiled-in
+// silhouette scan instead of silhouette_distance_compact.
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
-    return e ? (int)std::strtol(e, nullptr, 10) & 0xFFFF : 0;
+    return e ? (int)std::strtol(e, nullptr, 10) & 0xFFFFF : 0;
 }
 
 // the squared segment length exactly as the kernel forms it
@@ -391,10 +393,6 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     std::ostringstream o;
     if (exp_flags() & 2) o << "#define WOST_EXP_IEEE_DIRECTION 1\n";
     if (exp_flags() & 4096) o << "#define WOST_NO_TREE_BEHIND 1\n";   // A/B: line pruning only
-    // a tree kernel that stages the tree's top records in LDS (WOST_TREE_LDS, wider
-    // workgroups) reads records through generic pointers; the others use global loads
-    if (tree && block != kWalkBlock) o << "#define WOST_TREE_LDS_KERNEL 1\n";
-    if (tree && (exp_flags() & 8192)) o << "#define WOST_TREE_LDS_KERNEL 1\n";   // A/B: flat record loads
     if (exp_flags() & 4) o << "#define WOST_ABL_NO_PHILOX 1\n";
     if (exp_flags() & 8) o << "#define WOST_ABL_NO_ALPHA_Z 1\n";
     if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
@@ -471,7 +469,11 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         return v.str();
     };
     o << "    __device__ __forceinline__ float neumann_silhouette_distance(const float2* sN, int nn, float x, float y) const {\n";
-    if (nconst) o << nverts_decl() << "        return wost::silhouette_distance<" << nn << ">(v, " << nn << ", x, y);\n";
+    // 9+ compiled-in vertices: the two-pass scan (squared distances only for each
+    // lane's own silhouette vertices, from the staged copy)
+    if (nconst && nn >= 9 && nn <= 66 && !(exp_flags() & 32768))
+        o << nverts_decl() << "        return wost::silhouette_distance_compact<" << nn << ">(v, sN, x, y);\n";
+    else if (nconst) o << nverts_decl() << "        return wost::silhouette_distance<" << nn << ">(v, " << nn << ", x, y);\n";
     else o << "        return wost::silhouette_distance(sN, nn, x, y);\n";
     o << "    }\n";
     o << "    __device__ __forceinline__ wost::Hit neumann_intersect(const float2* sN, int nn, float x, float y, float dx,"
@@ -480,7 +482,12 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     // measured slower on C3's 32-segment circle: 1.24e10 vs 1.94e10 walk-steps/s)
     // 8+ compiled-in segments: the two-pass scan (C3's 32-segment circle +11%; with one or
     // two segments its loop costs more than it saves: C4 -9%, profiles/r02_ab/ray_scan_two_pass.log)
-    if (nconst && nn >= 9 && nn <= 65 && !(exp_flags() & 16384))   // (16384: per-segment exact tests, A/B)
+    if (nconst && nn >= 9 && nn <= 65 && !(exp_flags() & (16384 | 8192))) {   // the per-vertex line filter
+        float c1 = 0.0f;
+        for (int i = 0; i < nn; ++i) c1 = std::max(c1, std::fabs(nverts[2 * i]) + std::fabs(nverts[2 * i + 1]));
+        o << nverts_decl() << "        return wost::intersect_polylines_lines<" << nn << ">(v, sN, x, y, dx, dy, r, "
+          << lit(c1 * 1.0001f) << ");\n";
+    } else if (nconst && nn >= 9 && nn <= 65 && !(exp_flags() & 16384))   // (16384: per-segment exact tests, A/B)
         o << nverts_decl() << "        return wost::intersect_polylines_compact<" << nn << ">(v, sN, x, y, dx, dy, r);\n";
     else if (nconst && !(exp_flags() & 1024))   // (1024: the generic unroll-by-2 scan, A/B)
         o << nverts_decl() << "        return wost::intersect_polylines<false, " << nn << ">(v, " << nn

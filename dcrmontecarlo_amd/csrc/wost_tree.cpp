@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <limits>
 
 namespace wost {
@@ -37,81 +38,90 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
     if (nv < 2 || leaf < 1) return false;
     const int nseg = nv - 1;
     const int nleaves = (nseg + leaf - 1) / leaf;
-    int P = 1;
-    while (P < nleaves) P <<= 1;
-    const int n_nodes = 2 * P - 1;
-    out->first_leaf = P - 1;
+    int D = 1, P = 4;                       // leaves at level D, P = 4^D leaf slots
+    while (P < nleaves) { P *= 4; ++D; }
+    const int first_leaf = (P - 1) / 3;     // (4^D - 1) / 3 internal nodes
+    const int n_nodes = first_leaf + P;
+    out->first_leaf = first_leaf;
+    out->depth = D;
     out->leaf = leaf;
-    std::vector<float> node(8 * (size_t)n_nodes, 0.f);   // per node: box, cone
 
     // segment range [lo, hi] of every node (hi includes the right neighbour's
     // first segment: a vertex's silhouette test reads both adjacent segments)
     std::vector<int> lo(n_nodes, -1), hi(n_nodes, -1);
     for (int l = 0; l < P; ++l) {
-        const int k = P - 1 + l;
+        const int k = first_leaf + l;
         if (l * leaf < nseg) {
             lo[k] = l * leaf;
             hi[k] = std::min((l + 1) * leaf, nseg - 1);
         }
     }
-    for (int k = P - 2; k >= 0; --k) {
-        const int a = 2 * k + 1, b = 2 * k + 2;
-        if (lo[a] < 0) continue;
-        lo[k] = lo[a];
-        hi[k] = lo[b] < 0 ? hi[a] : hi[b];
+    for (int k = first_leaf - 1; k >= 0; --k) {
+        for (int j = 0; j < kTreeArity; ++j) {
+            const int c = kTreeArity * k + 1 + j;
+            if (lo[c] < 0) continue;
+            if (lo[k] < 0) lo[k] = lo[c];
+            hi[k] = hi[c];
+        }
     }
 
-    const float inf = std::numeric_limits<float>::infinity();
     float cmax = 0.f;
     for (int i = 0; i < 2 * nv; ++i) cmax = std::max(cmax, std::fabs(xy[i]));
-    out->tol = std::ldexp(1.0f + cmax, -14);
+    out->tol = std::ldexp(1.0f + cmax, -17);
 
+    // per node: the oriented box around the arc's axis and the arc (see the header)
+    std::vector<float> node((size_t)kTreeChildFloats * (size_t)n_nodes, 0.f);
     std::vector<double> ang;
-    for (int k = 0; k < n_nodes; ++k) {
-        float* box = &node[8 * (size_t)k];
-        float* cone = box + 4;
-        if (lo[k] < 0) {   // padding: inverted box, "no segment" cone
-            box[0] = inf; box[1] = inf; box[2] = -inf; box[3] = -inf;
-            cone[0] = 2.f; cone[1] = 0.f; cone[2] = 0.f; cone[3] = 0.f;
+    for (int k = 1; k < n_nodes; ++k) {   // (the root has no parent record)
+        float* o = &node[(size_t)kTreeChildFloats * (size_t)k];
+        if (lo[k] < 0) {                  // padding: never kept
+            o[0] = o[1] = 0.f; o[2] = 1.f; o[3] = 0.f; o[4] = -1.f; o[5] = -1.f; o[6] = 2.f; o[7] = 0.f;
             continue;
         }
-        float xmin = inf, ymin = inf, xmax = -inf, ymax = -inf;
-        for (int v = lo[k]; v <= hi[k] + 1; ++v) {
-            xmin = std::min(xmin, xy[2 * v]); xmax = std::max(xmax, xy[2 * v]);
-            ymin = std::min(ymin, xy[2 * v + 1]); ymax = std::max(ymax, xy[2 * v + 1]);
-        }
-        box[0] = xmin; box[1] = ymin; box[2] = xmax; box[3] = ymax;
-
         ang.clear();
-        for (int s = lo[k]; s <= hi[k]; ++s) {
-            const double ux = (double)xy[2 * s + 2] - xy[2 * s], uy = (double)xy[2 * s + 3] - xy[2 * s + 1];
+        for (int sg = lo[k]; sg <= hi[k]; ++sg) {
+            const double ux = (double)xy[2 * sg + 2] - xy[2 * sg], uy = (double)xy[2 * sg + 3] - xy[2 * sg + 1];
             if (ux != 0.0 || uy != 0.0) ang.push_back(std::atan2(uy, ux));
         }
         double axis = 0.0, half = 0.0;
-        if (!enclosing_arc(ang, &axis, &half)) {
-            cone[0] = 2.f; cone[1] = 0.f; cone[2] = 0.f; cone[3] = 0.f;   // only zero-length segments
-        } else if (half >= 0.5 * M_PI - 0.01) {
-            cone[0] = 3.f; cone[1] = 0.f; cone[2] = 0.f; cone[3] = 0.f;   // too wide to prune
+        int code = 0;
+        if (!enclosing_arc(ang, &axis, &half)) code = 2;                 // only zero-length segments
+        else if (half >= 0.5 * M_PI - 0.01) code = 3;                    // too wide to prune
+        // the box is built around the float axis the kernels read
+        const float fux = code == 0 ? (float)std::cos(axis) : 1.0f, fuy = code == 0 ? (float)std::sin(axis) : 0.0f;
+        const double ux = fux, uy = fuy, nx = -uy, ny = ux;
+        double tmin = 1e300, tmax = -1e300, smin = 1e300, smax = -1e300;
+        for (int v = lo[k]; v <= hi[k] + 1; ++v) {
+            const double x = xy[2 * v], y = xy[2 * v + 1];
+            const double tt = x * ux + y * uy, ss = x * nx + y * ny;
+            tmin = std::min(tmin, tt); tmax = std::max(tmax, tt);
+            smin = std::min(smin, ss); smax = std::max(smax, ss);
+        }
+        const double tc = 0.5 * (tmin + tmax), sc = 0.5 * (smin + smax);
+        const double cx = tc * ux + sc * nx, cy = tc * uy + sc * ny;
+        // inflate by far more than the rounding of the stored centre and of the
+        // kernels' corner arithmetic, so that the float box holds every vertex
+        const double slack = 16.0 * std::ldexp(1.0, -24) * (std::fabs(cx) + std::fabs(cy) + 0.5 * (tmax - tmin) +
+                                                             0.5 * (smax - smin)) + 1e-30;
+        const double a = (0.5 * (tmax - tmin) + slack) * (1.0 + std::ldexp(1.0, -20));
+        const double b = (0.5 * (smax - smin) + slack) * (1.0 + std::ldexp(1.0, -20));
+        o[0] = (float)cx; o[1] = (float)cy; o[2] = fux; o[3] = fuy; o[4] = (float)a; o[5] = (float)b;
+        if (code == 0) {
+            half += 1e-6;   // cover the float rounding of the axis and of the kernels' edge vectors
+            o[6] = (float)std::cos(half);
+            o[7] = (float)std::sin(half);
         } else {
-            half += 1e-6;   // cover the float rounding of the stored edges
-            cone[0] = (float)std::cos(axis - half);
-            cone[1] = (float)std::sin(axis - half);
-            cone[2] = (float)std::cos(axis + half);
-            cone[3] = (float)std::sin(axis + half);
+            o[6] = (float)code;
+            o[7] = 0.f;
         }
     }
-    // child records of the internal nodes: {box(2k+1), box(2k+2), cone(2k+1), cone(2k+2)}
-    out->rec.assign(16 * (size_t)(P - 1), 0.f);
-    for (int k = 0; k < P - 1; ++k) {
-        float* r = &out->rec[16 * (size_t)k];
-        for (int c = 0; c < 2; ++c) {
-            const float* nd = &node[8 * (size_t)(2 * k + 1 + c)];
-            for (int q = 0; q < 4; ++q) {
-                r[4 * c + q] = nd[q];          // box
-                r[8 + 4 * c + q] = nd[4 + q];  // cone
-            }
-        }
-    }
+    // child records of the internal nodes
+    out->rec.assign((size_t)kTreeNodeFloats * (size_t)first_leaf, 0.f);
+    for (int k = 0; k < first_leaf; ++k)
+        for (int j = 0; j < kTreeArity; ++j)
+            std::memcpy(&out->rec[(size_t)kTreeNodeFloats * k + (size_t)kTreeChildFloats * j],
+                        &node[(size_t)kTreeChildFloats * (size_t)(kTreeArity * k + 1 + j)],
+                        sizeof(float) * kTreeChildFloats);
     return true;
 }
 

@@ -7,16 +7,25 @@
 
 namespace wost {
 
+// floats per child description (oriented box + direction arc) and per internal node
+constexpr int kTreeChildFloats = 8;
+constexpr int kTreeArity = 4;
+constexpr int kTreeNodeFloats = kTreeArity * kTreeChildFloats;
+
 struct SegmentTreeHost {
-    std::vector<float> rec;    // 16 floats per internal node k: its children's boxes (xmin, ymin, xmax, ymax)
-                               // then their direction-arc edges (e1, e2): box(2k+1), box(2k+2), cone(2k+1), cone(2k+2)
+    std::vector<float> rec;    // kTreeNodeFloats per internal node k: for child j = 0..3 (node 4k+1+j)
+                               // {cx, cy, ux, uy, a, b, cos h, sin h}: the oriented box centred at c
+                               // with unit axis u, half-length a along u and half-width b across it,
+                               // and the half-angle h of the arc of segment directions around u
+                               // (cos h = 2: no segment direction; 3: arc too wide to use; a < 0: padding)
     int first_leaf = 0;        // index of the first leaf node = number of internal nodes
+    int depth = 0;             // level of the leaves (the root is level 0)
     int leaf = 0;              // segments per leaf
-    float tol = 0.f;           // line-test tolerance at the origin
+    float tol = 0.f;           // line-test tolerance at the origin; grows with |q|
 };
 
-// Builds the tree of the polyline xy[2*nv] (nv >= 2) with `leaf` segments per
-// leaf. Returns false for a degenerate input.
+// Builds the 4-ary tree of the polyline xy[2*nv] (nv >= 2) with `leaf` segments per
+// leaf (the leaf count padded to a power of 4). Returns false for a degenerate input.
 bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out);
 
 }  // namespace wost

@@ -48,8 +48,8 @@ struct WalkArgs {
     int32_t tree_leaf;
     float tree_tol;
     float tree_stop2;            // largest float whose sqrtf is <= rmin (< 0: none); silhouette_distance_tree
-    int32_t tree_lds_records;    // the first records of the tree staged in LDS (0: none)
-    int32_t pad_;
+    int32_t tree_lds_records;    // unused (0): the tree's records are read through L1/L2
+    int32_t tree_depth;          // level of the tree's leaves
     // walk-range batches (wost_solve_range): when range_walks > 0, local walk l is walk
     // range_offset + l % range_walks of point range_point0 + l / range_walks, i.e. global
     // id (range_point0 + l / range_walks) * walks_per_point + range_offset + l % range_walks
@@ -187,7 +187,6 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     lds += kStageN ? align16(sizeof(float2) * (size_t)A.nn) : 0;
     float* sPhi = reinterpret_cast<float*>(lds);
     lds += kStageN ? align16(sizeof(float) * (size_t)(A.nn > 1 ? A.nn - 1 : 0)) : 0;
-    float4* sTree = reinterpret_cast<float4*>(lds);
 
     if (kStageD)
         for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
@@ -195,14 +194,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
         for (int i = threadIdx.x; i < A.nn - 1; i += blockDim.x) sPhi[i] = A.seg_phi[i];
     }
-    if (TREE)   // the top levels of the segment tree (wost_device.h SegTree, child records)
-        for (int i = threadIdx.x; i < 4 * A.tree_lds_records; i += blockDim.x) sTree[i] = A.tree[i];
     // the polylines the queries read: the LDS copies, or (GL) global memory
     const float2* const dP = GL ? A.dverts : sD;
     const float2* const nP = GL ? A.nverts : sN;
     const float* const phiP = GL ? A.seg_phi : sPhi;
-    const SegTree tree{A.tree, TREE ? sTree : nullptr, TREE ? A.tree_lds_records : 0, A.nverts, A.nn,
-                       A.tree_first_leaf, A.tree_leaf, A.tree_tol};
+    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_depth, A.tree_leaf, A.tree_tol};
     float node0 = 0.0f;
     if (SRC) {
         node0 = A.table[0];

@@ -87,6 +87,18 @@ def flops_per_step(scenario) -> float:
     return F
 
 
+I0E_FLOPS = 120.0   # the i0e series SURVEY 8(d) counts in the delta-tracking overhead
+
+
+def executed_flops_per_step(scenario) -> float:
+    """The v1 model without the ~120 FLOP i0e series that delta tracking's step no
+    longer evaluates (the screened Green's norm is an LDS table lookup):
+    the FP32 work the kernel actually executes per step, by the same convention."""
+    f = flops_per_step(scenario)
+    delta = scenario.sigma is not None or scenario.alpha is not None
+    return f - I0E_FLOPS if delta else f
+
+
 def issue_fraction(valu_per_wave_step: float, trans_per_wave_step: float, steps_per_s: float) -> dict:
     """VALU issue-rate roofline: the SIMD cycles one wave-step's instructions occupy,
     (VALU - TRANS) x 2 + TRANS x 8, times the wave-steps per second, over the chip's

@@ -46,7 +46,7 @@ extern "C" {
 
 /* Neumann segment-tree defaults (wost_set_segment_tree). */
 #define WOST_TREE_MIN_SEGMENTS_DEFAULT 64
-#define WOST_TREE_LEAF_DEFAULT 8
+#define WOST_TREE_LEAF_DEFAULT 10
 
 enum wost_status {
     WOST_OK = 0,

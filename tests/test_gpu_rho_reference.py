@@ -87,9 +87,9 @@ def test_apparent_resistivity_replayed_reference_all_dipoles(gpu_available):
     replayed on the Philox stream at all 48 C4 electrodes x 400 walks, model conductivity
     and the alpha = 100 background (tests/golden/rho_replay_dcr_dipole.npz). The device on
     the same walks: every walk's step count identical, per-walk values within float
-    rounding, and all 47 dipoles' paired rho_a within 5e-4 relative of the reference's
-    (float rounding only: at 400 walks a dipole's dV can rest on a single walk, and one
-    walk's float32 rounding differs by up to ~1.4e-4 relative, test_oracle_golden)."""
+    rounding, and all 47 dipoles' paired rho_a within 1e-4 relative of the reference's
+    (measured 2.1e-7: the device's float32 fields round like the reference's; the CPU
+    oracle's double fields reach 1.4e-4, test_oracle_golden)."""
     from dcrmontecarlo_amd import scenarios as S
     from dcrmontecarlo_amd import survey
 
@@ -108,4 +108,4 @@ def test_apparent_resistivity_replayed_reference_all_dipoles(gpu_available):
     assert cmp["steps_identical"]
     assert cmp["walk_values_within_1e-4"] >= 0.99, cmp["walk_values_within_1e-4"]
     assert cmp["dipoles_compared"] == 47, cmp
-    assert cmp["rho_a_max_rel_diff"] <= 5e-4, (cmp["rho_a_max_rel_diff"], cmp["rho_a_gpu"], cmp["rho_a_reference"])
+    assert cmp["rho_a_max_rel_diff"] <= 1e-4, (cmp["rho_a_max_rel_diff"], cmp["rho_a_gpu"], cmp["rho_a_reference"])

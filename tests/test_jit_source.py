@@ -29,9 +29,11 @@ def test_generated_sources_name_their_variant():
     assert "wost::sat_sigmoid_lin(x, y, " in nb and nb.count("wost::sat_sigmoid_radial(x, y, ") == 2
     vc = S.variable_coefficients().kernel_source()          # detached alpha (Q9): no jet shortcut needed
     assert "if (WOST_SAT_ALL(sat))" not in vc
-    # 8+ compiled-in Neumann segments: the two-pass ray scan; C4's single top segment: the unrolled one
-    assert "intersect_polylines_compact<33>(v, sN," in vc
-    assert "intersect_polylines_compact" not in src and "intersect_polylines<false, 2>(v, 2," in src
+    # 8+ compiled-in Neumann segments: the two-pass scans (per-vertex line filter, marked
+    # silhouettes); C4's single top segment: the unrolled one
+    assert "intersect_polylines_lines<33>(v, sN," in vc and "silhouette_distance_compact<33>(v, sN," in vc
+    assert "intersect_polylines_lines" not in src and "intersect_polylines<false, 2>(v, 2," in src
+    assert "silhouette_distance<2>(v, 2," in src
     topo = S.wenner_topography(n_electrodes=4, n_walks=1).kernel_source()
     assert "walk_body<true, true, true, true, false, 1, false, false>" in topo      # the 10k-segment surface uses the tree
     lap = S.laplace_square().kernel_source()

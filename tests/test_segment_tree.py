@@ -127,9 +127,29 @@ def test_tree_early_stop_keeps_the_step_radius(harness, rmin):
     assert out[1] > 100, list(out)        # the early stop was exercised
 
 
-@pytest.mark.parametrize("shape", ["circle", "zigzag", "random_walk", "degenerate"])
+def test_tree_matches_scan_at_c5_walk_positions(harness):
+    """The positions C5 walks actually visit (30,000 steps recorded on the device by
+    tools/c5_paths.py: electrodes 0.1 below the surface, near-surface steps, walkers
+    escaped to |y| ~ 1e6), each with its Dirichlet distance, random directions and
+    the step radius: the tree's queries equal the full scans bit for bit."""
+    z = np.load(os.path.join(HERE, "golden", "c5_walk_positions.npz"))
+    rng = np.random.default_rng(11)
+    n = len(z["points"])
+    th = rng.random(n) * 2 * np.pi
+    dirs = np.stack([np.cos(th), np.sin(th)], 1)
+    radii = np.minimum(z["dd"], 10.0 ** rng.uniform(-1, 3, n))
+    for leaf in (8, 10, 16):
+        counts = run(harness, S.topography(10_000), z["points"], dirs, radii, z["dd"], leaf=leaf)
+        assert counts[0] == 0 and counts[1] == 0, (leaf, counts)
+        assert counts[2] > 100 and counts[3] > 1000, counts
+
+
+SHAPES = ["circle", "zigzag", "random_walk", "degenerate", "far_offset"]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
 def test_tree_matches_scan_shapes(harness, shape):
-    rng = np.random.default_rng(["circle", "zigzag", "random_walk", "degenerate"].index(shape))
+    rng = np.random.default_rng(SHAPES.index(shape))
     if shape == "circle":                                   # closed, every vertex a silhouette candidate
         th = np.linspace(0, 2 * np.pi, 513)
         verts = np.stack([40 * np.cos(th), 40 * np.sin(th)], 1)
@@ -138,9 +158,11 @@ def test_tree_matches_scan_shapes(harness, shape):
         verts = np.stack([x, np.where(np.arange(801) % 2, 1.0, -1.0)], 1)
     elif shape == "random_walk":
         verts = np.cumsum(rng.normal(size=(1500, 2)), 0)
-    else:                                                   # repeated vertices, zero-length segments
+    elif shape == "degenerate":                             # repeated vertices, zero-length segments
         x = np.repeat(np.linspace(-10, 10, 300), 2)
         verts = np.stack([x, np.sin(x)], 1)
+    else:                                                   # large coordinates: the tolerances scale
+        verts = S.topography(3000).astype(np.float64) + np.array([3.0e4, -2.0e4])
     verts = verts.astype(np.float32)
     counts = run(harness, verts, *queries(rng, verts, 40000))
     assert counts[0] == 0 and counts[1] == 0, counts

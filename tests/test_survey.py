@@ -107,13 +107,13 @@ def test_homogeneous_scenario_keeps_survey():
 
 @pytest.mark.gpu
 def test_gpu_survey_rho_a_matches_cpu_oracle(gpu_available):
-    """Reduced C4 survey (12 electrodes around the sources x 2000 walks): rho_a on
+    """Reduced C4 survey (12 electrodes around the sources x 16000 walks): rho_a on
     the GPU vs the CPU oracle on the same walks. The walks agree one for one up to
     the scenario's chaos (~1-2% diverge), so the rho_a RMSE is a small fraction of
     the Monte-Carlo 1-sigma (the north-star bound is RMSE <= 1 sigma)."""
     from oracle import oracle as O
 
-    sc = S.dcr_dipole(n_electrodes=48, n_walks=2000)
+    sc = S.dcr_dipole(n_electrodes=48, n_walks=16000)
     sc.points = sc.points[18:30]          # x = -16.5 .. 16.5: around the two sources
     alpha_bg = 100.0
     res = survey.run_dipole_dipole(sc, alpha_bg, sc.n_walks, seed=5, device=0)

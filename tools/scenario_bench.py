@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Walk-steps/s of every scenario kernel variant on one GPU (device time of the walk
 kernel from libwost's HIP events, plus wall time of the solve). Honours WOST_LIB.
-Usage: python tools/scenario_bench.py [--scale 1.0] [--only a,b]"""
+With --cpu, the CPU oracle (oracle/wost_oracle.c, the reference's algorithm with its
+brute-force scans, OpenMP over walks) runs a bounded sample of the same scenario on
+every usable host core and on one core, beside the GPU number.
+Usage: python tools/scenario_bench.py [--scale 1.0] [--only a,b] [--cpu [--cpu-seconds 3]]"""
 import argparse
 import json
 import os
@@ -16,8 +19,39 @@ from dcrmontecarlo_amd import scenarios as S  # noqa: E402
 SIZES = {
     "laplace_square": (64, 200_000), "manufactured_polynomial": (16, 500_000), "poisson_square": (64, 200_000),
     "variable_coefficients": (256, 20_000), "dcr_dipole": (48, 1_000_000), "notebook_dcr": (21, 200_000),
-    "wenner_topography": (256, 2000),
+    "wenner_topography": (256, 2000), "wenner_topography_physical": (256, 2000),
 }
+
+
+def cpu_rate(sc, pts, sigma_bar, budget_s):
+    """The oracle on a bounded sample of the scenario's walks: (all-core rate, cores,
+    sample, one-core rate, sample)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import oracle as O
+    from bench import host_cpu
+
+    info = host_cpu()
+    threads = info["affinity_cpus"]
+    if info["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(round(info["cgroup_cpu_quota"]))))
+    pb = O.Problem.from_scenario(sc, sigma_bar=sigma_bar or 0.0)
+    pb.solve_walks(pts[:1], 1, sc.max_steps, sc.eps, 1, threads=1)
+    w = 1
+    while True:
+        t0 = time.perf_counter()
+        _, st = pb.solve_walks(pts, w, sc.max_steps, sc.eps, 7, threads=threads)
+        dt = time.perf_counter() - t0
+        if dt >= 0.3 * budget_s or w >= 1 << 20:
+            break
+        w = int(min(1 << 20, w * max(2.0, 0.6 * budget_s / max(dt, 1e-4))))
+    all_rate = float(st.sum()) / dt
+    w1 = max(1, w // max(threads, 1))
+    t0 = time.perf_counter()
+    _, s1 = pb.solve_walks(pts, w1, sc.max_steps, sc.eps, 8, threads=1)
+    dt1 = time.perf_counter() - t0
+    return {"cpu_walk_steps_per_s": all_rate, "cpu_cores": threads, "cpu_sample": f"{len(pts)} pts x {w} walks, {dt:.1f} s",
+            "cpu1_walk_steps_per_s": float(s1.sum()) / dt1, "cpu1_sample": f"{len(pts)} pts x {w1} walks, {dt1:.1f} s",
+            "cpu_model": info["cpu_model"]}
 
 
 def main():
@@ -27,6 +61,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--compat", default="reference", help="reference | fixed")
     ap.add_argument("--scan", action="store_true", help="force the full Neumann scans (no segment tree)")
+    ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle on a bounded sample")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0)
     a = ap.parse_args()
     names = a.only.split(",") if a.only else list(SIZES)
     out = {}
@@ -51,7 +87,7 @@ def main():
                 best = rec
         # C5's segment tree is reported as a speed-up over the brute-force scan, never as a
         # roofline fraction
-        fps = perfmodel.flops_per_step(sc) if (sc.name != "wenner_topography" or a.scan) else None
+        fps = perfmodel.flops_per_step(sc) if (not sc.name.startswith("wenner_topography") or a.scan) else None
         best["steps_per_s_kernel"] = best["steps"] / (best["kernel_ms"] * 1e-3)
         best["steps_per_s_wall"] = best["steps"] / best["wall_s"]
         best["model_tflops"] = fps * best["steps_per_s_kernel"] / 1e12 if fps else float("nan")
@@ -59,9 +95,15 @@ def main():
         best["mean_steps"] = best["steps"] / (npts * W)
         best["config"] = f"{npts} pts x {W} walks"
         out[name] = best
+        cpu = ""
+        if a.cpu and a.compat == "reference":
+            best.update(cpu_rate(sc, pts, solver.sigma_bar, a.cpu_seconds))
+            cpu = (f" | CPU oracle {best['cpu_walk_steps_per_s']:.3e} on {best['cpu_cores']} cores "
+                   f"({best['cpu_sample']}), {best['cpu1_walk_steps_per_s']:.3e} on 1 core; GPU/CPU "
+                   f"{best['steps_per_s_kernel'] / best['cpu_walk_steps_per_s']:.0f}x")
         print(f"{name:26s} {best['config']:22s} {best['steps_per_s_kernel']:.3e} steps/s (kernel) "
               f"{best['steps_per_s_wall']:.3e} (wall) {best['model_tflops']:.1f} TF ({100*best['frac_fp32']:.1f}%) "
-              f"grid {best['grid']} mean steps {best['mean_steps']:.1f}", flush=True)
+              f"grid {best['grid']} mean steps {best['mean_steps']:.1f}{cpu}", flush=True)
     print("JSON " + json.dumps(out))
 
 
