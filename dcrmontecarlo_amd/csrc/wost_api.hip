@@ -524,7 +524,7 @@ int create_host(const wost_problem* pb, wost_handle** out) {
     h->compat = pb->compat;
     if (const char* e = std::getenv("WOST_JIT")) h->jit_enabled = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("WOST_TREE_MIN_SEGMENTS")) h->tree_min_segments = std::atoi(e);
-    if (const char* e = std::getenv("WOST_TREE_LEAF")) h->tree_leaf = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("WOST_TREE_LEAF")) h->tree_leaf = std::min(32, std::max(1, std::atoi(e)));
     // solvers/WoStSolver.py:54-64: any of sigma/alpha turns on delta tracking,
     // the missing one defaults to sigma = 0 / alpha = 1 (constant => Q9 fallback).
     h->delta = h->fields[SLOT_SIGMA].present || h->fields[SLOT_ALPHA].present;
@@ -1119,7 +1119,7 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
 
 int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments) {
     if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
-    if (leaf_segments < 0) return fail(WOST_ERR_INVALID_ARG, "leaf_segments must be >= 0");
+    if (leaf_segments < 0 || leaf_segments > 32) return fail(WOST_ERR_INVALID_ARG, "leaf_segments must be in [0, 32]");
     h->tree_min_segments = min_segments;
     if (leaf_segments > 0 && leaf_segments != h->tree_leaf) {
         h->tree_leaf = leaf_segments;

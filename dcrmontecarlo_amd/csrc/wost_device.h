@@ -1509,20 +1509,36 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
         WOST_TREE_COUNT(3);
         const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
-        if (s0 < s1) {
+        if (NEAREST && s0 < s1) {
             float2 a = t.v[s0];
             for (int i = s0; i < s1; ++i) {
                 const float2 b = t.v[i + 1];
-                if (NEAREST) {
-                    // t <= best (ties too: the lower segment index wins them)
-                    const float bq = best < WOST_INF ? bits_to_float(__builtin_bit_cast(int32_t, best) + 1) : best;   // t > 0
-                    const float tt = ray_segment_nearest_t(a, b, qx, qy, dx, dy, bq);
-                    if (tt < best || (tt == best && i < bi)) { best = tt; bi = i; }
-                } else {
-                    const float s = ray_segment_time_filtered(a, b, qx, qy, dx, dy);
-                    if (s < best || (s == best && i < bi)) { best = s; bi = i; }
-                }
+                // t <= best (ties too: the lower segment index wins them)
+                const float bq = best < WOST_INF ? bits_to_float(__builtin_bit_cast(int32_t, best) + 1) : best;   // t > 0
+                const float tt = ray_segment_nearest_t(a, b, qx, qy, dx, dy, bq);
+                if (tt < best || (tt == best && i < bi)) { best = tt; bi = i; }
                 a = b;
+            }
+        } else if (s0 < s1) {
+            // candidates by the per-vertex line filter of intersect_polylines_lines (S =
+            // 2 tol >= 2^-17 (max_i |v_i|_1 + |q|_1)), then each lane's own candidates
+            // through the exact test; a leaf holds at most 32 segments
+            const float S = 2.0f * tol;
+            const float m = fmaf(dx, qy, -(dy * qx));
+            float2 a = t.v[s0];
+            float ca = fmaf(dx, a.y, -(dy * a.x)) - m;
+            uint32_t cand = 0u;
+            for (int i = s0; i < s1; ++i) {
+                const float2 b = t.v[i + 1];
+                const float cb = fmaf(dx, b.y, -(dy * b.x)) - m;
+                if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) cand |= 1u << (i - s0);
+                ca = cb;
+            }
+            while (cand != 0u) {
+                const int i = s0 + lowest_bit(cand);
+                cand &= cand - 1u;
+                const float s = ray_segment_time_filtered(t.v[i], t.v[i + 1], qx, qy, dx, dy);
+                if (s < best || (s == best && i < bi)) { best = s; bi = i; }
             }
         }
         live = resume();

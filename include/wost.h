@@ -371,8 +371,8 @@ int wost_set_jit(wost_handle* h, int32_t enable);
  * segments (default WOST_TREE_MIN_SEGMENTS_DEFAULT; < 0: never, 0: always)
  * the walk kernel's closest-silhouette and ray queries (geometry/
  * PolylinesSimple.py:83-102, :134-197, which scan every segment) go through an
- * implicit bounding-box / normal-cone tree with leaf_segments segments per
- * leaf (0 keeps the current value), under both estimators (compat="fixed":
+ * implicit 4-ary tree of oriented boxes and direction arcs with leaf_segments
+ * (1..32) segments per leaf (0 keeps the current value), under both estimators (compat="fixed":
  * the nearest-crossing ray query). Results are bit-identical to the scans.
  * Environment: WOST_TREE_MIN_SEGMENTS, WOST_TREE_LEAF. */
 int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments);
