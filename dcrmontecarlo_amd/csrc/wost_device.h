@@ -1346,22 +1346,40 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     uint32_t pend = 0u;     // 4 bits per level: children of that level's node still to visit
     // test the children `cand` of node (lvl, at) against the bound: the kept ones,
     // and the nearest of them in `nj`
-    auto visit = [&](int lvl, int at, uint32_t cand, int& nj) {
+    // the smallest lower bound among the pending children of each of the first five
+    // levels: a level whose pending children all lie beyond the tightened bound is
+    // dropped on resume without reloading its record (deeper levels are re-tested)
+    float plb0 = WOST_INF, plb1 = WOST_INF, plb2 = WOST_INF, plb3 = WOST_INF, plb4 = WOST_INF;
+    auto plb_get = [&](int l) {
+        float v = -WOST_INF;
+        v = l == 0 ? plb0 : v; v = l == 1 ? plb1 : v; v = l == 2 ? plb2 : v;
+        v = l == 3 ? plb3 : v; v = l == 4 ? plb4 : v;
+        return v;
+    };
+    auto plb_set = [&](int l, float x) {
+        plb0 = l == 0 ? x : plb0; plb1 = l == 1 ? x : plb1; plb2 = l == 2 ? x : plb2;
+        plb3 = l == 3 ? x : plb3; plb4 = l == 4 ? x : plb4;
+    };
+    // test the children `cand` of node (lvl, at) against the bound: the kept ones,
+    // the nearest of them in `nj`, and the smallest lower bound of the others in nb2
+    auto visit = [&](int lvl, int at, uint32_t cand, int& nj, float& nb2) {
         const int k = tree_level_offset(lvl) + at;
         const float bound = best < T ? best : T;
         uint32_t kept = 0u;
         float nb = WOST_INF;
+        nb2 = WOST_INF;
         nj = 0;
+        WOST_TREE_COUNT(0);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             if (!((cand >> j) & 1u)) continue;
-            WOST_TREE_COUNT(0);
             const float4 cu = t.word(k, 2 * j), ab = t.word(k, 2 * j + 1);
             const ChildFrame f = child_frame(cu, px, py);
             const float lb = box_lower_bound2(ab, f);
             if (!(lb > bound) && !cone_excludes_silhouettes(ab, f)) {
                 kept |= 1u << j;
-                if (lb < nb) { nb = lb; nj = j; }
+                if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
+                else if (lb < nb2) nb2 = lb;
             }
         }
         return kept;
@@ -1373,11 +1391,15 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
             const int p = highest_bit(pend) >> 2;
             const uint32_t m = (pend >> (4 * p)) & 15u;
             pend &= ~(15u << (4 * p));
+            const float bound = best < T ? best : T;
+            if (plb_get(p) > bound) continue;   // every pending child of this level is pruned
             const int anc = pos >> (2 * (d - p));
             int nj;
-            const uint32_t kept = visit(p, anc, m, nj);
+            float nb2;
+            const uint32_t kept = visit(p, anc, m, nj, nb2);
             if (kept) {
                 pend |= (kept & ~(1u << nj)) << (4 * p);
+                plb_set(p, nb2);
                 pos = 4 * anc + nj;
                 d = p + 1;
                 return true;
@@ -1391,9 +1413,11 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     while (live) {
         while (live && d < t.depth) {
             int nj;
-            const uint32_t kept = visit(d, pos, 15u, nj);
+            float nb2;
+            const uint32_t kept = visit(d, pos, 15u, nj, nb2);
             if (kept) {
                 pend |= (kept & ~(1u << nj)) << (4 * d);
+                plb_set(d, nb2);
                 pos = 4 * pos + nj;
                 ++d;
             } else {

@@ -33,29 +33,33 @@ float g_margin = 1e-5f;
 float g_tolscale = 1.0f;
 
 int g_pow4 = 0;
+int g_arity = 2;
 
 bool build_obb(const float* xy, int nv, int leaf, ObbTree* t) {
     const int nseg = nv - 1;
     const int nleaves = (nseg + leaf - 1) / leaf;
-    int P = 1;
-    while (P < nleaves) P <<= (g_pow4 ? 2 : 1);
-    const int n_nodes = 2 * P - 1;
-    t->first_leaf = P - 1;
+    const int A = g_arity;
+    int P = A;
+    while (P < nleaves) P *= A;
+    const int first_leaf = (P - 1) / (A - 1);
+    const int n_nodes = first_leaf + P;
+    t->first_leaf = first_leaf;
     t->leaf = leaf;
     t->v = reinterpret_cast<const float2*>(xy);
     t->nv = nv;
     t->nd.assign(8 * (size_t)n_nodes, 0.f);
     std::vector<int> lo(n_nodes, -1), hi(n_nodes, -1);
     for (int l = 0; l < P; ++l) {
-        const int k = P - 1 + l;
+        const int k = first_leaf + l;
         if (l * leaf < nseg) { lo[k] = l * leaf; hi[k] = std::min((l + 1) * leaf, nseg - 1); }
     }
-    for (int k = P - 2; k >= 0; --k) {
-        const int a = 2 * k + 1, b = 2 * k + 2;
-        if (lo[a] < 0) continue;
-        lo[k] = lo[a];
-        hi[k] = lo[b] < 0 ? hi[a] : hi[b];
-    }
+    for (int k = first_leaf - 1; k >= 0; --k)
+        for (int j = 0; j < A; ++j) {
+            const int c = A * k + 1 + j;
+            if (lo[c] < 0) continue;
+            if (lo[k] < 0) lo[k] = lo[c];
+            hi[k] = hi[c];
+        }
     float cmax = 0.f;
     for (int i = 0; i < 2 * nv; ++i) cmax = std::max(cmax, std::fabs(xy[i]));
     t->tol = std::ldexp(1.0f + cmax, -14);
@@ -267,10 +271,10 @@ float sil_obb4(const ObbTree& t, float px, float py, float dd, float stop2, long
         if (lb > bound) continue;
         if (k < t.first_leaf) {
             ++cnt[0];
-            std::pair<float, int> ch[4];
+            std::pair<float, int> ch[64];
             int nk = 0;
-            for (int j = 0; j < 4; ++j) {
-                const int c = 4 * k + 3 + j;
+            for (int j = 0; j < g_arity; ++j) {
+                const int c = g_arity * k + 1 + j;
                 const float* o = node(t, c);
                 const float l = obb_lb2(o, px, py);
                 if (!(l > bound) && !obb_cone_excludes(o, px, py)) ch[nk++] = {l, c};
@@ -336,7 +340,7 @@ Hit ray_obb4(const ObbTree& t, float px, float py, float dxi, float dyi, float r
         st.pop_back();
         if (k < t.first_leaf) {
             ++cnt[2];
-            for (int j = 3; j >= 0; --j) if (keep(node(t, 4 * k + 3 + j))) st.push_back(4 * k + 3 + j);
+            for (int j = g_arity - 1; j >= 0; --j) if (keep(node(t, g_arity * k + 1 + j))) st.push_back(g_arity * k + 1 + j);
             continue;
         }
         ++cnt[3];
@@ -370,7 +374,7 @@ int obb_counts(const float* xy, int nv, int leaf, float margin, const float* pts
                float rmin, float stop2, long n, long* out, long* mism, int arity) {
     ObbTree t;
     g_margin = margin;
-    g_pow4 = arity == 4;
+    g_arity = arity;
     if (getenv("TOLSCALE")) g_tolscale = atof(getenv("TOLSCALE"));
     build_obb(xy, nv, leaf, &t);
     const float2* v = reinterpret_cast<const float2*>(xy);
@@ -379,13 +383,13 @@ int obb_counts(const float* xy, int nv, int leaf, float margin, const float* pts
         long* c = out + 4 * i;
         c[0] = c[1] = c[2] = c[3] = 0;
         const float px = pts[2 * i], py = pts[2 * i + 1];
-        const float dn_t = arity == 4 ? sil_obb4(t, px, py, dd[i], stop2, c) : sil_obb(t, px, py, dd[i], stop2, c);
+        const float dn_t = arity > 2 ? sil_obb4(t, px, py, dd[i], stop2, c) : sil_obb(t, px, py, dd[i], stop2, c);
         const float dn_b = silhouette_distance(v, nv, px, py);
         const float mb = dn_b < dd[i] ? dn_b : dd[i], mt = dn_t < dd[i] ? dn_t : dd[i];
         const float rb = mb > rmin ? mb : rmin, rt = mt > rmin ? mt : rmin;
         if (!same(rb, rt)) ++mism[0];
         const Hit hb = intersect_polylines(v, nv, px, py, dirs[2 * i], dirs[2 * i + 1], rb);
-        const Hit ht = arity == 4 ? ray_obb4(t, px, py, dirs[2 * i], dirs[2 * i + 1], rb, c)
+        const Hit ht = arity > 2 ? ray_obb4(t, px, py, dirs[2 * i], dirs[2 * i + 1], rb, c)
                                   : ray_obb(t, px, py, dirs[2 * i], dirs[2 * i + 1], rb, c);
         if (!same(hb.x, ht.x) || !same(hb.y, ht.y) || hb.hit != ht.hit || (hb.hit && hb.seg != ht.seg)) {
             if (mism[1] < 3)
