@@ -44,7 +44,8 @@ namespace {
 // (intersect_polylines_compact) instead of the per-vertex line filter
 // (intersect_polylines_lines); 16384 the per-segment exact tests instead of either
 // two-pass scan for 8+ compiled-in segments; 32768 the one-pass compiled-in
-// silhouette scan instead of silhouette_distance_compact.
+// silhouette scan instead of silhouette_distance_compact; ablation 65536 no tree
+// silhouette query (dn = +inf).
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
@@ -397,6 +398,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 8) o << "#define WOST_ABL_NO_ALPHA_Z 1\n";
     if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
     if (exp_flags() & 32) o << "#define WOST_ABL_NO_RAY 1\n";
+    if (exp_flags() & 65536) o << "#define WOST_ABL_NO_SILHOUETTE 1\n";
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";

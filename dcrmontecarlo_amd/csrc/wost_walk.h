@@ -347,8 +347,12 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
         if (NEU) {
+#if defined(WOST_ABL_NO_SILHOUETTE)   // ablation (timing only)
+            const float dn = TREE ? WOST_INF : fld.neumann_silhouette_distance(nP, A.nn, px, py);
+#else
             const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
                                   : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
+#endif
             dnv = dn;
             const float m = dn < dd ? dn : dd;                       // Python min()
             r = m > A.rmin ? m : A.rmin;                             // Python max() (:212)
