@@ -1297,37 +1297,27 @@ WOST_HD int tree_level_offset(int d) { return (int)(((1u << (2 * d)) - 1u) / 3u)
 // b cos h, with a margin of 1e-5 |p - q|_1, some 20 times the rounding of these
 // values and of any c_i. (The same bound the eight corner cross products give, in
 // six operations.)
-struct ChildFrame {
-    float wx, wy, pu, pn;
-};
-
-WOST_HD ChildFrame child_frame(float4 cu, float px, float py) {
+// One child's silhouette test: *lb = the box lower bound (+inf for padding); true
+// when the child is kept (lb within the bound and the cone test cannot exclude it).
+// The cone condition cos h |pn| - sin h |pu| > a sin h + b cos h + margin is
+// evaluated as cos h (|pn| - b) - sin h (|pu| + a) > margin, sharing |pn| - b and
+// |pu| - a with the bound; the margin (1e-5 (|w|_1 + 2(a + b))) stays ~40 times
+// the rounding of either form.
+WOST_HD bool silhouette_child_keep(float4 cu, float4 ab, float px, float py, float bound, float* lb) {
 #pragma clang fp contract(off)
-    ChildFrame f;
-    f.wx = px - cu.x;
-    f.wy = py - cu.y;
-    f.pu = f.wx * cu.z + f.wy * cu.w;
-    f.pn = f.wy * cu.z - f.wx * cu.w;
-    return f;
-}
-
-WOST_HD float box_lower_bound2(float4 ab, const ChildFrame& f) {
-#pragma clang fp contract(off)
-    if (ab.x < 0.0f) return WOST_INF;
-    const float sl = 9.5367431640625e-07f * ((fabsf(f.wx) + fabsf(f.wy)) + (ab.x + ab.y));   // 2^-20
-    float gu = (fabsf(f.pu) - ab.x) - sl, gn = (fabsf(f.pn) - ab.y) - sl;
+    const float wx = px - cu.x, wy = py - cu.y;
+    const float pu = wx * cu.z + wy * cu.w, pn = wy * cu.z - wx * cu.w;
+    const float W = fabsf(wx) + fabsf(wy), AB = ab.x + ab.y;
+    const float au = fabsf(pu), en = fabsf(pn) - ab.y;
+    const float sl = 9.5367431640625e-07f * (W + AB);                   // 2^-20
+    float gu = (au - ab.x) - sl, gn = en - sl;
     gu = gu > 0.0f ? gu : 0.0f;
     gn = gn > 0.0f ? gn : 0.0f;
-    return (gu * gu + gn * gn) * 0.99999904632568359375f;   // 1 - 2^-20
-}
-
-WOST_HD bool cone_excludes_silhouettes(float4 ab, const ChildFrame& f) {
-#pragma clang fp contract(off)
-    if (ab.z == 2.0f) return true;
-    if (ab.z == 3.0f) return false;
-    const float K = (ab.x * ab.w + ab.y * ab.z) * 1.00000095367431640625f;   // a sin h + b cos h, rounded up
-    const float m = kConeMargin * ((fabsf(f.wx) + fabsf(f.wy)) + (ab.x + ab.y) * 2.0f);
-    return ab.z * fabsf(f.pn) - ab.w * fabsf(f.pu) > m + K;
+    const float l = ab.x < 0.0f ? WOST_INF : (gu * gu + gn * gn) * 0.99999904632568359375f;   // 1 - 2^-20
+    *lb = l;
+    if (l > bound || ab.z == 2.0f) return false;
+    if (ab.z == 3.0f) return true;
+    return !(ab.z * en - ab.w * (au + ab.x) > kConeMargin * (W + AB * 2.0f));
 }
 
 // silhouette_distance for the use r = max(rmin, min(dn, dd)) of :210-212: exact
@@ -1374,9 +1364,8 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
         for (int j = 0; j < 4; ++j) {
             if (!((cand >> j) & 1u)) continue;
             const float4 cu = t.word(k, 2 * j), ab = t.word(k, 2 * j + 1);
-            const ChildFrame f = child_frame(cu, px, py);
-            const float lb = box_lower_bound2(ab, f);
-            if (!(lb > bound) && !cone_excludes_silhouettes(ab, f)) {
+            float lb;
+            if (silhouette_child_keep(cu, ab, px, py, bound, &lb)) {
                 kept |= 1u << j;
                 if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
                 else if (lb < nb2) nb2 = lb;
