@@ -3,7 +3,10 @@
 rocprofv3 PMC passes of tools/profile_session.sh: VALU and transcendental VALU
 instructions per wave-step of the walk kernel (SQ_INSTS_VALU, SQ_INSTS_VALU_TRANS_F32
 per dispatch, over walk-steps / 64).
-Usage: tools/issue_json.py <pmc_sq1 dir> <pmc_trans dir> <walk-steps per dispatch> <source label>"""
+Usage: tools/issue_json.py <pmc_sq1 dir> <pmc_trans dir> <walk-steps per dispatch> <source label>
+                           [<scenario> [<pmc dir with SQ_THREAD_CYCLES_VALU, SQ_ACTIVE_INST_VALU>]]
+(scenario default dcr_dipole -> profiles/issue_<scenario>.json; with the third dir the
+lane utilisation SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU) is recorded too)"""
 import csv
 import json
 import os
@@ -21,14 +24,22 @@ def per_dispatch(d, counter):
 def main():
     valu = per_dispatch(sys.argv[1], "SQ_INSTS_VALU")
     trans = per_dispatch(sys.argv[2], "SQ_INSTS_VALU_TRANS_F32")
+    if len(sys.argv) > 5:   # a scenario_bench run: a warm-up launch, then the measured one (the largest)
+        i = max(range(len(valu)), key=lambda j: valu[j])
+        valu, trans = [valu[i]], [trans[max(range(len(trans)), key=lambda j: trans[j])]]
     steps = float(sys.argv[3])
     ws = steps / 64.0
-    out = {"kernel": "wost_walk_jit (dcr_dipole, 48 x 1M walks)", "dispatches": [len(valu), len(trans)],
+    sc = sys.argv[5] if len(sys.argv) > 5 else "dcr_dipole"
+    out = {"kernel": f"wost_walk_jit ({sc})", "dispatches": [len(valu), len(trans)],
            "walk_steps_per_dispatch": steps,
            "valu_per_wave_step": sum(valu) / len(valu) / ws, "trans_per_wave_step": sum(trans) / len(trans) / ws,
            "source": sys.argv[4] + " (rocprofv3 --pmc SQ_INSTS_VALU / SQ_INSTS_VALU_TRANS_F32, separate passes)"}
+    if len(sys.argv) > 6:
+        tc = per_dispatch(sys.argv[6], "SQ_THREAD_CYCLES_VALU")
+        ai = per_dispatch(sys.argv[6], "SQ_ACTIVE_INST_VALU")
+        out["lane_utilisation"] = max(tc) / (64.0 * max(ai))
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                        "issue_dcr_dipole.json")
+                        f"issue_{sc}.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))
