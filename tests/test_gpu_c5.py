@@ -6,13 +6,15 @@ the CPU oracle (geometry/PolylinesSimple.py:25-49, :83-102, :134-197).
 * every step of recorded device walks: the Dirichlet distance and the Neumann
   silhouette distance the tree kernel used equal the oracle's full scans bit for
   bit (the tree must not change a single query);
-* device vs oracle on the same Philox streams (16 electrodes x 256 walks): a
-  chaos-aware walk-agreement floor -- the oracle against itself under a 1-ulp
-  direction perturbation agrees on 86.5% of these walks (their Q1 Neumann "hits"
-  make C5 the most chaotic scenario) -- and per-electrode means within 3
-  combined standard errors;
+* device vs oracle on the same Philox streams (32 electrodes x 512 walks): the
+  walks that agree must be at least as many as those the oracle keeps against
+  ITSELF under a 1-ulp perturbation of the step direction, measured on the same
+  walks in the same test (their Q1 Neumann "hits" make C5 the most chaotic
+  scenario: ~87% self-agreement), less 2 points; and per-electrode means within
+  3 combined standard errors;
 * full size (256 electrodes x 10k walks): u(2f) = 2 u(f) bit for bit, and the tree
-  kernel equals the brute-force scan kernel walk for walk on a subset;
+  kernel equals the brute-force scan kernel walk for walk on 64 electrodes x 256
+  walks (~3.4M steps through both kernels);
 * the Wenner survey's multi-source batching equals per-source solves bit for bit.
 """
 import numpy as np
@@ -20,7 +22,6 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-AGREEMENT_FLOOR_C5 = 0.80
 
 
 def _c5(**kw):
@@ -59,14 +60,22 @@ def test_c5_device_matches_oracle(gpu_available):
 
     sc = _c5()
     s = sc.solver(device=0)
-    pts = sc.points[8::16][:16]
-    W = 256
+    pts = sc.points[4::8][:32]
+    W = 512
     gv, gs = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=31337)
     gv, gs = gv.ravel(), gs.ravel()
-    ov, os_ = O.Problem.from_scenario(sc, sigma_bar=s.sigma_bar).solve_walks(pts, W, sc.max_steps, sc.eps, 31337)
+    pb = O.Problem.from_scenario(sc, sigma_bar=s.sigma_bar)
+    ov, os_ = pb.solve_walks(pts, W, sc.max_steps, sc.eps, 31337)
+    try:
+        O.set_direction_perturbation(1.2e-7)       # 1 ulp of the step direction
+        pv, ps = pb.solve_walks(pts, W, sc.max_steps, sc.eps, 31337)
+    finally:
+        O.set_direction_perturbation(0.0)
     scale = max(float(np.abs(ov).max()), 1e-30)
-    same = (gs == os_) & (np.abs(gv - ov) <= 1e-3 * np.abs(ov) + 1e-5 * scale)
-    assert same.mean() >= AGREEMENT_FLOOR_C5, same.mean()
+    agree = lambda v, st: (st == os_) & (np.abs(v - ov) <= 1e-3 * np.abs(ov) + 1e-5 * scale)
+    chaos = agree(pv, ps).mean()                   # the oracle against itself, 1 ulp apart
+    device = agree(gv, gs).mean()
+    assert chaos > 0.5 and device >= chaos - 0.02, (device, chaos)
     g = gv.astype(np.float64).reshape(len(pts), W)
     o = ov.astype(np.float64).reshape(len(pts), W)
     se = np.sqrt(g.var(1, ddof=1) / W + o.var(1, ddof=1) / W)
@@ -88,10 +97,10 @@ def test_c5_full_size_linearity_and_tree_equals_scan(gpu_available):
     assert np.array_equal(st2.mean, 2.0 * st1.mean)
     assert st1.total_steps == st2.total_steps > 256 * 10_000 * 50
     # the tree kernel against the brute-force scan kernel, walk for walk, on a subset
-    sub = sc.points[::32]
-    tv, ts = s1.solve_walks(sub, nWalks=64, maxSteps=sc.max_steps, eps=sc.eps, seed=23)
+    sub = sc.points[::4]
+    tv, ts = s1.solve_walks(sub, nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=23)
     s1.set_segment_tree(-1)
-    bv, bs = s1.solve_walks(sub, nWalks=64, maxSteps=sc.max_steps, eps=sc.eps, seed=23)
+    bv, bs = s1.solve_walks(sub, nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=23)
     assert s1.last_timing["tree"] == 0
     np.testing.assert_array_equal(ts, bs)
     np.testing.assert_array_equal(tv.view(np.uint32), bv.view(np.uint32))
