@@ -404,6 +404,10 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
     if (const char* e = std::getenv("WOST_JIT_REFILL_MIN"))   // A/B: refill batch size
         o << "#define WOST_REFILL_MIN " << std::max(1, std::min(64, std::atoi(e))) << "\n";
+    if (const char* e = std::getenv("WOST_JIT_TREE_SHARE"))   // A/B: tree hand-out threshold (0: none)
+        o << "#define WOST_TREE_SHARE " << std::max(0, std::min(64, std::atoi(e))) << "\n";
+    if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_DESCENT"))   // A/B: hand-outs during the descent
+        o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";

@@ -92,13 +92,22 @@ enum RecField { REC_X = 0, REC_Y, REC_DD, REC_DN, REC_SX, REC_SY, REC_C, REC_AUX
 
 WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
+// LDS scratch of one wave for the cooperative tree queries (below): the hand-out
+// slots and one result slot per owner lane
+struct TreeWaveScratch {
+    uint32_t task[64];             // owner | level << 6 | position << 10
+    unsigned long long slot[64];   // silhouette: float bits of the squared distance; ray: s bits << 32 | segment
+};
+constexpr size_t kTreeWaveScratchBytes = sizeof(TreeWaveScratch);
+
 // Bytes of dynamic LDS a walk-kernel workgroup needs, in layout order:
 //  * G_norm cells (delta tracking; else a 16-byte pad): sample_rho_tail reads the
 //    word before the sampler's tail;
 //  * the sampler's nodes 1..N-1 (node 0 is a kernel argument);
 //  * the Dirichlet vertices, unless the Fields policy has them compiled in;
 //  * the Neumann vertices and segment angles (scan kernels), unless compiled in;
-//  * with the segment tree, its first tree_lds records (64 B each).
+//  * with the segment tree, its first tree_lds records (64 B each), then one
+//    TreeWaveScratch per wave (the cooperative tree queries).
 // Query points are read from global memory (once per walk, at refill).
 WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false,
                                   bool delta = false, int tree_lds = 0, bool const_d = false, bool const_n = false,
@@ -112,8 +121,381 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
     if (!const_d) b += align16(sizeof(float2) * (size_t)nd);
     if (neu && !tree && !const_n)
         b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
-    if (tree) b += 4 * sizeof(float4) * (size_t)tree_lds;
+    if (tree) b += 4 * sizeof(float4) * (size_t)tree_lds + kTreeWaveScratchBytes * (size_t)(kWalkBlock / 64);
     return b;
+}
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative segment-tree queries (TREE kernels, reference mode).
+//
+// silhouette_distance_tree / intersect_polylines_tree run one query per lane, and a
+// wave iterates until its slowest lane is done: at C5's walk positions ~89% of the
+// queries end after one or two record visits while the few near the surface need
+// 20-40, so a tree instruction ran on ~12-19% of the lanes. Here the lanes of a wave
+// share the work: when at most WOST_TREE_SHARE lanes still search, the searching
+// lanes hand the subtrees pending in their traversal state (pend bits: the children
+// of an ancestor still to visit) to idle lanes, which search them for the same query
+// (the owner's registers, read with a lane shuffle) and leave their result in the
+// owner's LDS slot. Both queries are minima that do not depend on the visiting order
+// (the silhouette query's squared distance, the ray query's lexicographic (s, segment)
+// -- the scan's first argmin), so the answer is bit for bit the per-lane search's.
+// Shared bounds only prune more: at each hand-out the silhouette searches of one
+// owner take the smallest squared distance found so far by any of them.
+// Every lane of the wave calls these together (no lane may have left the loop body).
+// ---------------------------------------------------------------------------
+#ifndef WOST_TREE_SHARE   // hand out pending subtrees when at most this many lanes search
+#define WOST_TREE_SHARE 16
+#endif
+#ifndef WOST_TREE_SHARE_DESCENT   // also at every level of the descent (else once per leaf round)
+#define WOST_TREE_SHARE_DESCENT 0
+#endif
+
+
+// the LDS writes of the wave's lanes visible to its other lanes (a wave's LDS
+// operations complete in order; this keeps the compiler from moving them)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// exclusive prefix sum over the wave of n < 32, and the total, from five ballots
+__device__ __forceinline__ uint32_t wave_prefix32(uint32_t n, uint64_t lanes_below, uint32_t* total) {
+    uint32_t off = 0u, tot = 0u;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+        const uint64_t m = __ballot((n >> b) & 1u);
+        off += (uint32_t)__popcll(m & lanes_below) << b;
+        tot += (uint32_t)__popcll(m) << b;
+    }
+    *total = tot;
+    return off;
+}
+
+// Hand out pending subtrees: searching lanes (`live`) list their pend bits (the
+// shallowest levels, i.e. the largest subtrees, first) into the idle lanes' slots;
+// an idle lane that receives one becomes a helper: *owner, d, pos of the subtree's
+// root, pend = 0. Returns true on the lanes that became helpers.
+__device__ __forceinline__ bool tree_hand_out(TreeWaveScratch* ws, uint64_t live_mask, bool live,
+                                              uint64_t lanes_below, int& owner, int& d, int& pos, uint32_t& pend) {
+    const uint64_t idle = ~live_mask;
+    const uint32_t nidle = (uint32_t)__popcll(idle);
+    uint32_t ntot;
+    const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
+    const uint32_t off = wave_prefix32(n, lanes_below, &ntot);
+    if (live && off < nidle) {
+        const uint32_t give = n < nidle - off ? n : nidle - off;
+        for (uint32_t i = 0; i < give; ++i) {
+            const int b = lowest_bit(pend);
+            pend &= pend - 1u;
+            const int p = b >> 2, child = 4 * (pos >> (2 * (d - p))) + (b & 3);
+            ws->task[off + i] = (uint32_t)owner | (uint32_t)(p + 1) << 6 | (uint32_t)child << 10;
+        }
+    }
+    wave_lds_sync();
+    const uint32_t rank = (uint32_t)__popcll(idle & lanes_below);
+    const bool helper = !live && rank < (ntot < nidle ? ntot : nidle);
+    if (helper) {
+        const uint32_t tk = ws->task[rank];
+        owner = (int)(tk & 63u);
+        d = (int)((tk >> 6) & 15u);
+        pos = (int)(tk >> 10);
+        pend = 0u;
+    }
+    return helper;
+}
+
+// silhouette_distance_tree (wost_device.h), the wave's lanes sharing the search;
+// `want`: this lane has a query. Same use contract (exact below dd and above rmin).
+__device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t, float px, float py, float dd,
+                                                               float stop2, bool want, TreeWaveScratch* ws,
+                                                               int lane) {
+#pragma clang fp contract(off)
+    const uint64_t lanes_below = (1ull << lane) - 1ull;
+    const int nv = t.nv, nseg = nv - 1;
+    const float Town = (dd * dd) * 1.002f;
+    ws->slot[lane] = (unsigned long long)__builtin_bit_cast(uint32_t, WOST_INF);
+    // the query this lane searches for (its own, or its owner's as a helper)
+    float qx = px, qy = py, T = Town;
+    int owner = lane;
+    float best = WOST_INF;
+    bool live = want && nv >= 3;
+    int d = 0, pos = 0;
+    uint32_t pend = 0u;
+    float plb0 = WOST_INF, plb1 = WOST_INF, plb2 = WOST_INF, plb3 = WOST_INF, plb4 = WOST_INF;
+    auto plb_get = [&](int l) {
+        float v = -WOST_INF;
+        v = l == 0 ? plb0 : v; v = l == 1 ? plb1 : v; v = l == 2 ? plb2 : v;
+        v = l == 3 ? plb3 : v; v = l == 4 ? plb4 : v;
+        return v;
+    };
+    auto plb_set = [&](int l, float x) {
+        plb0 = l == 0 ? x : plb0; plb1 = l == 1 ? x : plb1; plb2 = l == 2 ? x : plb2;
+        plb3 = l == 3 ? x : plb3; plb4 = l == 4 ? x : plb4;
+    };
+    auto visit = [&](int lvl, int at, uint32_t cand, int& nj, float& nb2) {
+        const int k = tree_level_offset(lvl) + at;
+        const float bound = best < T ? best : T;
+        uint32_t kept = 0u;
+        float nb = WOST_INF;
+        nb2 = WOST_INF;
+        nj = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!((cand >> j) & 1u)) continue;
+            const float4 cu = t.word(k, 2 * j), ab = t.word(k, 2 * j + 1);
+            float lb;
+            if (silhouette_child_keep(cu, ab, qx, qy, bound, &lb)) {
+                kept |= 1u << j;
+                if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
+                else if (lb < nb2) nb2 = lb;
+            }
+        }
+        return kept;
+    };
+    auto resume = [&]() {
+        while (pend != 0u) {
+            const int p = highest_bit(pend) >> 2;
+            const uint32_t m = (pend >> (4 * p)) & 15u;
+            pend &= ~(15u << (4 * p));
+            const float bound = best < T ? best : T;
+            if (plb_get(p) > bound) continue;
+            const int anc = pos >> (2 * (d - p));
+            int nj;
+            float nb2;
+            const uint32_t kept = visit(p, anc, m, nj, nb2);
+            if (kept) {
+                pend |= (kept & ~(1u << nj)) << (4 * p);
+                plb_set(p, nb2);
+                pos = 4 * anc + nj;
+                d = p + 1;
+                return true;
+            }
+        }
+        return false;
+    };
+    // hand out pending subtrees when few lanes still search (a uniform branch)
+    auto share = [&](uint64_t L) {
+        if (!(__popcll(L) <= WOST_TREE_SHARE && __ballot(live && pend != 0u) != 0ull)) return;
+        // every lane leaves what it found in its owner's slot, then takes the owner's
+        // best so far as its bound
+        if (best < WOST_INF) atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
+        if (tree_hand_out(ws, L, live, lanes_below, owner, d, pos, pend)) {
+            live = true;
+            best = WOST_INF;
+            plb0 = plb1 = plb2 = plb3 = plb4 = WOST_INF;
+        }
+        qx = __shfl(px, owner);
+        qy = __shfl(py, owner);
+        T = __shfl(Town, owner);
+        const float sb = __builtin_bit_cast(float, (uint32_t)ws->slot[owner]);
+        best = sb < best ? sb : best;
+        if (live && best <= stop2) { live = false; pend = 0u; }
+    };
+    wave_lds_sync();
+    for (;;) {
+        const uint64_t L = __ballot(live);
+        if (L == 0ull) break;
+        share(L);
+#if WOST_TREE_SHARE_DESCENT
+        // the descent as a uniform loop, so that a hand-out can run at every level
+        for (;;) {
+            const bool down = live && d < t.depth;
+            if (!__any(down)) break;
+            if (down) {
+#else
+        {
+            while (live && d < t.depth) {
+#endif
+                int nj;
+                float nb2;
+                const uint32_t kept = visit(d, pos, 15u, nj, nb2);
+                if (kept) {
+                    pend |= (kept & ~(1u << nj)) << (4 * d);
+                    plb_set(d, nb2);
+                    pos = 4 * pos + nj;
+                    ++d;
+                } else {
+                    live = resume();
+                }
+            }
+#if WOST_TREE_SHARE_DESCENT
+            share(__ballot(live));
+#endif
+        }
+        // (no `continue` in this loop: every lane must reach the next ballot)
+        if (live) {
+            const int s0 = pos * t.leaf;
+            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+            const int j1 = s1 < nv - 2 ? s1 : nv - 2;
+            bool stop = false;
+            if (s0 + 1 <= j1) {
+                const float2 va = t.v[s0];
+                float2 vb = t.v[s0 + 1];
+                float cprev = (vb.x - va.x) * (qy - va.y) - (vb.y - va.y) * (qx - va.x);
+                for (int j = s0 + 1; j <= j1; ++j) {
+                    const float2 vc = t.v[j + 1];
+                    const float bpx = qx - vb.x, bpy = qy - vb.y;
+                    const float ccur = (vc.x - vb.x) * bpy - (vc.y - vb.y) * bpx;
+                    if (cprev * ccur < 0.0f) {
+                        const float d2 = bpx * bpx + bpy * bpy;
+                        best = d2 < best ? d2 : best;
+                    }
+                    cprev = ccur;
+                    vb = vc;
+                }
+                stop = best <= stop2;
+            }
+            if (stop) {
+                live = false;
+                pend = 0u;
+            } else {
+                live = resume();
+            }
+        }
+    }
+    if (best < WOST_INF) atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
+    wave_lds_sync();
+    const float res = __builtin_bit_cast(float, (uint32_t)ws->slot[lane]);
+    wave_lds_sync();   // the slots are rewritten by the next query
+    return res == WOST_INF ? res : sqrt_rn(res);
+}
+
+// intersect_polylines_tree<NORMAL> (wost_device.h, reference mode), the wave's lanes
+// sharing the search; `want`: this lane has a query.
+template <bool NORMAL = true>
+__device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, float px, float py, float dxi,
+                                                             float dyi, float r, bool want, TreeWaveScratch* ws,
+                                                             int lane) {
+#pragma clang fp contract(off)
+    const uint64_t lanes_below = (1ull << lane) - 1ull;
+    float dn, dx, dy;
+    unit_direction(dxi, dyi, dn, dx, dy);
+    const bool degenerate = dn < 1e-10f;
+    const float qx0 = px + 1e-6f * dx, qy0 = py + 1e-6f * dy;
+    const float tol0 = t.tol + 7.62939453125e-06f * (fabsf(qx0) + fabsf(qy0));   // + 2^-17 |q|_1
+    const int nseg = t.nv - 1;
+    ws->slot[lane] = ~0ull;
+    float qx = qx0, qy = qy0, ddx = dx, ddy = dy, tol = tol0;
+    int owner = lane;
+    float best = WOST_INF;
+    int bi = -1;
+    bool live = want && !degenerate;
+    // the pruning of intersect_polylines_tree's keep()
+    auto keep = [&](float4 cu, float4 ab) {
+        if (ab.x < 0.0f) return false;
+        const float cx = cu.x - qx, cy = cu.y - qy;
+        const float cr = ddx * cu.w - ddy * cu.z, dt = ddx * cu.z + ddy * cu.w;
+        if (fabsf(ddx * cy - ddy * cx) > (ab.x * fabsf(cr) + ab.y * fabsf(dt)) + tol) return false;
+#if !defined(WOST_NO_TREE_BEHIND)
+        if (ab.z == 3.0f) return true;
+        const float ahead = (ddx * cx + ddy * cy) + (ab.x * fabsf(dt) + ab.y * fabsf(cr));
+        if (!(ahead < -(512.0f * tol + 1e-2f * ((fabsf(cx) + fabsf(cy)) + (ab.x + ab.y))))) return true;
+        if (ab.z == 2.0f) return false;
+        return !(ab.z * fabsf(cr) - ab.w * fabsf(dt) > 1e-3f);
+#else
+        return true;
+#endif
+    };
+    int d = 0, pos = 0;
+    uint32_t pend = 0u;
+    auto resume = [&]() {
+        if (pend == 0u) return false;
+        const int p = highest_bit(pend) >> 2;
+        const int j = lowest_bit((pend >> (4 * p)) & 15u);
+        pend &= ~(1u << (4 * p + j));
+        pos = 4 * (pos >> (2 * (d - p))) + j;
+        d = p + 1;
+        return true;
+    };
+    // (s, segment) as one 64-bit key: s >= 0 here, so its bits order like the floats
+    // (s + 0 makes a -0 the +0 it ties with, leaving the segment index to decide)
+    auto deposit = [&]() {
+        if (bi >= 0)
+            atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best + 0.0f) << 32 |
+                                            (unsigned long long)(uint32_t)bi);
+    };
+    auto share = [&](uint64_t L) {
+        if (!(__popcll(L) <= WOST_TREE_SHARE && __ballot(live && pend != 0u) != 0ull)) return;
+        deposit();
+        if (tree_hand_out(ws, L, live, lanes_below, owner, d, pos, pend)) {
+            live = true;
+            best = WOST_INF;
+            bi = -1;
+        }
+        qx = __shfl(qx0, owner);
+        qy = __shfl(qy0, owner);
+        ddx = __shfl(dx, owner);
+        ddy = __shfl(dy, owner);
+        tol = __shfl(tol0, owner);
+    };
+    wave_lds_sync();
+    for (;;) {
+        const uint64_t L = __ballot(live);
+        if (L == 0ull) break;
+        share(L);
+#if WOST_TREE_SHARE_DESCENT
+        for (;;) {
+            const bool down = live && d < t.depth;
+            if (!__any(down)) break;
+            if (down) {
+#else
+        {
+            while (live && d < t.depth) {
+#endif
+                const int k = tree_level_offset(d) + pos;
+                uint32_t kept = 0u;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (keep(t.word(k, 2 * j), t.word(k, 2 * j + 1))) kept |= 1u << j;
+                if (kept) {
+                    const int j = lowest_bit(kept);
+                    pend |= (kept & ~(1u << j)) << (4 * d);
+                    pos = 4 * pos + j;
+                    ++d;
+                } else {
+                    live = resume();
+                }
+            }
+#if WOST_TREE_SHARE_DESCENT
+            share(__ballot(live));
+#endif
+        }
+        const int s0 = pos * t.leaf;
+        const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+        if (live && s0 < s1) {
+            const float S = 2.0f * tol;
+            const float m = fmaf(ddx, qy, -(ddy * qx));
+            float2 a = t.v[s0];
+            float ca = fmaf(ddx, a.y, -(ddy * a.x)) - m;
+            uint32_t cand = 0u;
+            for (int i = s0; i < s1; ++i) {
+                const float2 b = t.v[i + 1];
+                const float cb = fmaf(ddx, b.y, -(ddy * b.x)) - m;
+                if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) cand |= 1u << (i - s0);
+                ca = cb;
+            }
+            while (cand != 0u) {
+                const int i = s0 + lowest_bit(cand);
+                cand &= cand - 1u;
+                const float s = ray_segment_time_filtered(t.v[i], t.v[i + 1], qx, qy, ddx, ddy);
+                if (s < best || (s == best && i < bi)) { best = s; bi = i; }
+            }
+        }
+        if (live) live = resume();
+    }
+    deposit();
+    wave_lds_sync();
+    const unsigned long long key = ws->slot[lane];
+    wave_lds_sync();   // the slots are rewritten by the next query
+    if (degenerate) {
+        Hit h;
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
+        return h;
+    }
+    const int wbi = key == ~0ull ? -1 : (int)(uint32_t)key;
+    const float wbest = key == ~0ull ? WOST_INF : __builtin_bit_cast(float, (uint32_t)(key >> 32));
+    return intersect_finish<NORMAL>(t.v, wbi, wbest, px, py, dx, dy, qx0, qy0, r);
 }
 
 // The Fields policy F provides: has_g(), g(x,y), f(x,y), sigma(x,y),
@@ -187,6 +569,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     lds += kStageN ? align16(sizeof(float2) * (size_t)A.nn) : 0;
     float* sPhi = reinterpret_cast<float*>(lds);
     lds += kStageN ? align16(sizeof(float) * (size_t)(A.nn > 1 ? A.nn - 1 : 0)) : 0;
+    // the cooperative tree queries (reference mode; compat="fixed" keeps the per-lane ones)
+    constexpr bool kWaveTree = TREE && !FIX;
+    TreeWaveScratch* const tws = reinterpret_cast<TreeWaveScratch*>(lds + 4 * sizeof(float4) * (size_t)A.tree_lds_records) +
+                                 (threadIdx.x >> 6);
 
     if (kStageD)
         for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
@@ -336,7 +722,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         if (!__any(active)) break;
         // a freshly refilled walk may already fail the while-condition (eps >= 1,
         // maxSteps == 0): it takes no step and is finished at the next iteration
-        if (!(active && (k < A.max_steps) && (dD > A.eps))) continue;
+        const bool stepping = active && (k < A.max_steps) && (dD > A.eps);
+        // the cooperative tree queries need every lane of the wave: the others run the
+        // step's pure arithmetic up to the ray query with them and leave after it
+        if (kWaveTree ? !__any(stepping) : !stepping) continue;
 
         // --- one walk-step (:206-291)
         const float dd = fld.dirichlet_distance(dP, A.nd, px, py);  // :208
@@ -350,8 +739,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #if defined(WOST_ABL_NO_SILHOUETTE)   // ablation (timing only)
             const float dn = TREE ? WOST_INF : fld.neumann_silhouette_distance(nP, A.nn, px, py);
 #else
-            const float dn = TREE ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
-                                  : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
+            const float dn = kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane)
+                           : TREE      ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
+                                       : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
 #endif
             dnv = dn;
             const float m = dn < dd ? dn : dd;                       // Python min()
@@ -387,9 +777,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #else
             const Hit h = FIX ? (TREE ? intersect_polylines_tree<false, true>(tree, px, py, cs, sn, r)
                                       : fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r))
-                              : TREE ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
-                                     : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
+                              : kWaveTree ? intersect_polylines_tree_wave<false>(tree, px, py, cs, sn, r, stepping, tws, lane)
+                              : TREE      ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
+                                          : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
 #endif
+            if (kWaveTree && !stepping) continue;   // the lanes that only helped
             xnx = h.x; xny = h.y; onB = h.hit;
             if (h.hit) phi = TREE ? A.seg_phi[h.seg] : fld.neumann_phi(phiP, h.seg);
             if (FIX && h.hit) {
