@@ -408,6 +408,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_TREE_SHARE " << std::max(0, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_DESCENT"))   // A/B: hand-outs during the descent
         o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
+    if (const char* e = std::getenv("WOST_JIT_TREE_BATCH"))   // A/B: children loaded per batch
+        o << "#define WOST_TREE_BATCH " << (std::atoi(e) >= 4 ? 4 : std::atoi(e) >= 2 ? 2 : 1) << "\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
@@ -516,7 +518,10 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "        return sPhi[seg];\n";
     }
     o << "    }\n};\n}  // namespace\n\n";
-    int waves = 6;   // waves per SIMD the register budget is sized for (tools/ab_bench.sh)
+    // waves per SIMD the register budget is sized for (tools/ab_bench.sh): 6, or 5 for the
+    // cooperative tree kernels, whose record visits load four children's words at once
+    // (profiles/r03_tree/tree_batch_waves_ab.log)
+    int waves = (tree && !mode_fix(mode)) ? 5 : 6;
     if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
     o << "extern \"C\" __global__ void __launch_bounds__(" << block << ", " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"

@@ -144,10 +144,13 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 // Every lane of the wave calls these together (no lane may have left the loop body).
 // ---------------------------------------------------------------------------
 #ifndef WOST_TREE_SHARE   // hand out pending subtrees when at most this many lanes search
-#define WOST_TREE_SHARE 16
+#define WOST_TREE_SHARE 32
 #endif
 #ifndef WOST_TREE_SHARE_DESCENT   // also at every level of the descent (else once per leaf round)
-#define WOST_TREE_SHARE_DESCENT 0
+#define WOST_TREE_SHARE_DESCENT 1
+#endif
+#ifndef WOST_TREE_BATCH   // children of a record whose words are loaded together (1, 2 or 4)
+#define WOST_TREE_BATCH 4
 #endif
 
 
@@ -240,15 +243,23 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
         float nb = WOST_INF;
         nb2 = WOST_INF;
         nj = 0;
+        // the children's words loaded WOST_TREE_BATCH children at a time before any test
+        // (one round trip per batch; tested one by one the loads waited in turn)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (!((cand >> j) & 1u)) continue;
-            const float4 cu = t.word(k, 2 * j), ab = t.word(k, 2 * j + 1);
-            float lb;
-            if (silhouette_child_keep(cu, ab, qx, qy, bound, &lb)) {
-                kept |= 1u << j;
-                if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
-                else if (lb < nb2) nb2 = lb;
+        for (int j0 = 0; j0 < 4; j0 += WOST_TREE_BATCH) {
+            float4 w[2 * WOST_TREE_BATCH];
+#pragma unroll
+            for (int i = 0; i < 2 * WOST_TREE_BATCH; ++i) w[i] = t.word(k, 2 * j0 + i);
+#pragma unroll
+            for (int u = 0; u < WOST_TREE_BATCH; ++u) {
+                const int j = j0 + u;
+                float lb;
+                const bool keep = silhouette_child_keep(w[2 * u], w[2 * u + 1], qx, qy, bound, &lb);
+                if (((cand >> j) & 1u) && keep) {
+                    kept |= 1u << j;
+                    if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
+                    else if (lb < nb2) nb2 = lb;
+                }
             }
         }
         return kept;
@@ -333,16 +344,25 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
                 const float2 va = t.v[s0];
                 float2 vb = t.v[s0 + 1];
                 float cprev = (vb.x - va.x) * (qy - va.y) - (vb.y - va.y) * (qx - va.x);
-                for (int j = s0 + 1; j <= j1; ++j) {
-                    const float2 vc = t.v[j + 1];
-                    const float bpx = qx - vb.x, bpy = qy - vb.y;
-                    const float ccur = (vc.x - vb.x) * bpy - (vc.y - vb.y) * bpx;
-                    if (cprev * ccur < 0.0f) {
-                        const float d2 = bpx * bpx + bpy * bpy;
-                        best = d2 < best ? d2 : best;
+                // vertices loaded four at a time (indices clamped in range), then scanned
+                for (int j0 = s0 + 1; j0 <= j1; j0 += 4) {
+                    float2 vcs[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) vcs[u] = t.v[j0 + 1 + u < nv ? j0 + 1 + u : nv - 1];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (j0 + u <= j1) {
+                            const float2 vc = vcs[u];
+                            const float bpx = qx - vb.x, bpy = qy - vb.y;
+                            const float ccur = (vc.x - vb.x) * bpy - (vc.y - vb.y) * bpx;
+                            if (cprev * ccur < 0.0f) {
+                                const float d2 = bpx * bpx + bpy * bpy;
+                                best = d2 < best ? d2 : best;
+                            }
+                            cprev = ccur;
+                            vb = vc;
+                        }
                     }
-                    cprev = ccur;
-                    vb = vc;
                 }
                 stop = best <= stop2;
             }
@@ -446,8 +466,14 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
                 const int k = tree_level_offset(d) + pos;
                 uint32_t kept = 0u;
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (keep(t.word(k, 2 * j), t.word(k, 2 * j + 1))) kept |= 1u << j;
+                for (int j0 = 0; j0 < 4; j0 += WOST_TREE_BATCH) {
+                    float4 w[2 * WOST_TREE_BATCH];
+#pragma unroll
+                    for (int i = 0; i < 2 * WOST_TREE_BATCH; ++i) w[i] = t.word(k, 2 * j0 + i);
+#pragma unroll
+                    for (int u = 0; u < WOST_TREE_BATCH; ++u)
+                        if (keep(w[2 * u], w[2 * u + 1])) kept |= 1u << (j0 + u);
+                }
                 if (kept) {
                     const int j = lowest_bit(kept);
                     pend |= (kept & ~(1u << j)) << (4 * d);
@@ -466,14 +492,21 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         if (live && s0 < s1) {
             const float S = 2.0f * tol;
             const float m = fmaf(ddx, qy, -(ddy * qx));
-            float2 a = t.v[s0];
+            const float2 a = t.v[s0];
             float ca = fmaf(ddx, a.y, -(ddy * a.x)) - m;
             uint32_t cand = 0u;
-            for (int i = s0; i < s1; ++i) {
-                const float2 b = t.v[i + 1];
-                const float cb = fmaf(ddx, b.y, -(ddy * b.x)) - m;
-                if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) cand |= 1u << (i - s0);
-                ca = cb;
+            for (int i0 = s0; i0 < s1; i0 += 4) {   // vertices loaded four at a time
+                float2 bs[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) bs[u] = t.v[i0 + 1 + u <= nseg ? i0 + 1 + u : nseg];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (i0 + u < s1) {
+                        const float cb = fmaf(ddx, bs[u].y, -(ddy * bs[u].x)) - m;
+                        if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) cand |= 1u << (i0 + u - s0);
+                        ca = cb;
+                    }
+                }
             }
             while (cand != 0u) {
                 const int i = s0 + lowest_bit(cand);
