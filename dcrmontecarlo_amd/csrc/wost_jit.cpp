@@ -408,6 +408,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_TREE_SHARE " << std::max(0, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_DESCENT"))   // A/B: hand-outs during the descent
         o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
+    if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_MIN"))   // A/B: fewest subtrees worth a hand-out
+        o << "#define WOST_TREE_SHARE_MIN " << std::max(1, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_BATCH"))   // A/B: children loaded per batch
         o << "#define WOST_TREE_BATCH " << (std::atoi(e) >= 4 ? 4 : std::atoi(e) >= 2 ? 2 : 1) << "\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"

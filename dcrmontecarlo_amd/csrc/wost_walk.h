@@ -149,6 +149,9 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 #ifndef WOST_TREE_SHARE_DESCENT   // also at every level of the descent (else once per leaf round)
 #define WOST_TREE_SHARE_DESCENT 1
 #endif
+#ifndef WOST_TREE_SHARE_MIN   // ... and at least this many subtrees are pending
+#define WOST_TREE_SHARE_MIN 1
+#endif
 #ifndef WOST_TREE_BATCH   // children of a record whose words are loaded together (1, 2 or 4)
 #define WOST_TREE_BATCH 4
 #endif
@@ -162,30 +165,36 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// exclusive prefix sum over the wave of n < 32, and the total, from five ballots
-__device__ __forceinline__ uint32_t wave_prefix32(uint32_t n, uint64_t lanes_below, uint32_t* total) {
-    uint32_t off = 0u, tot = 0u;
+// The pending subtrees of the wave: per bit b of each lane's count n < 32 of pend
+// bits, the ballot of that bit (so the total is scalar work and a lane's prefix
+// offset is taken only when a hand-out happens).
+struct PendCount {
+    uint64_t m[5];
+    uint32_t total;
+};
+__device__ __forceinline__ PendCount wave_pend_count(uint32_t n) {
+    PendCount c;
+    c.total = 0u;
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
-        const uint64_t m = __ballot((n >> b) & 1u);
-        off += (uint32_t)__popcll(m & lanes_below) << b;
-        tot += (uint32_t)__popcll(m) << b;
+        c.m[b] = __ballot((n >> b) & 1u);
+        c.total += (uint32_t)__popcll(c.m[b]) << b;
     }
-    *total = tot;
-    return off;
+    return c;
 }
 
-// Hand out pending subtrees: searching lanes (`live`) list their pend bits (the
-// shallowest levels, i.e. the largest subtrees, first) into the idle lanes' slots;
-// an idle lane that receives one becomes a helper: *owner, d, pos of the subtree's
-// root, pend = 0. Returns true on the lanes that became helpers.
-__device__ __forceinline__ bool tree_hand_out(TreeWaveScratch* ws, uint64_t live_mask, bool live,
-                                              uint64_t lanes_below, int& owner, int& d, int& pos, uint32_t& pend) {
+// Hand out pending subtrees: searching lanes (`live`, n = popcount(pend)) list their
+// pend bits (the shallowest levels, i.e. the largest subtrees, first) into the idle
+// lanes' slots; an idle lane that receives one becomes a helper: *owner, d, pos of the
+// subtree's root, pend = 0. Returns true on the lanes that became helpers.
+__device__ __forceinline__ bool tree_hand_out(TreeWaveScratch* ws, uint64_t live_mask, bool live, uint32_t n,
+                                              const PendCount& pc, uint64_t lanes_below, int& owner, int& d, int& pos,
+                                              uint32_t& pend) {
     const uint64_t idle = ~live_mask;
     const uint32_t nidle = (uint32_t)__popcll(idle);
-    uint32_t ntot;
-    const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
-    const uint32_t off = wave_prefix32(n, lanes_below, &ntot);
+    uint32_t off = 0u;   // exclusive prefix sum of n over the lanes below
+#pragma unroll
+    for (int b = 0; b < 5; ++b) off += (uint32_t)__popcll(pc.m[b] & lanes_below) << b;
     if (live && off < nidle) {
         const uint32_t give = n < nidle - off ? n : nidle - off;
         for (uint32_t i = 0; i < give; ++i) {
@@ -197,7 +206,7 @@ __device__ __forceinline__ bool tree_hand_out(TreeWaveScratch* ws, uint64_t live
     }
     wave_lds_sync();
     const uint32_t rank = (uint32_t)__popcll(idle & lanes_below);
-    const bool helper = !live && rank < (ntot < nidle ? ntot : nidle);
+    const bool helper = !live && rank < (pc.total < nidle ? pc.total : nidle);
     if (helper) {
         const uint32_t tk = ws->task[rank];
         owner = (int)(tk & 63u);
@@ -287,11 +296,14 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
     };
     // hand out pending subtrees when few lanes still search (a uniform branch)
     auto share = [&](uint64_t L) {
-        if (!(__popcll(L) <= WOST_TREE_SHARE && __ballot(live && pend != 0u) != 0ull)) return;
+        if (!(__popcll(L) <= WOST_TREE_SHARE)) return;
+        const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
+        const PendCount pc = wave_pend_count(n);
+        if (pc.total < WOST_TREE_SHARE_MIN) return;
         // every lane leaves what it found in its owner's slot, then takes the owner's
         // best so far as its bound
         if (best < WOST_INF) atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
-        if (tree_hand_out(ws, L, live, lanes_below, owner, d, pos, pend)) {
+        if (tree_hand_out(ws, L, live, n, pc, lanes_below, owner, d, pos, pend)) {
             live = true;
             best = WOST_INF;
             plb0 = plb1 = plb2 = plb3 = plb4 = WOST_INF;
@@ -436,9 +448,12 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
                                             (unsigned long long)(uint32_t)bi);
     };
     auto share = [&](uint64_t L) {
-        if (!(__popcll(L) <= WOST_TREE_SHARE && __ballot(live && pend != 0u) != 0ull)) return;
+        if (!(__popcll(L) <= WOST_TREE_SHARE)) return;
+        const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
+        const PendCount pc = wave_pend_count(n);
+        if (pc.total < WOST_TREE_SHARE_MIN) return;
         deposit();
-        if (tree_hand_out(ws, L, live, lanes_below, owner, d, pos, pend)) {
+        if (tree_hand_out(ws, L, live, n, pc, lanes_below, owner, d, pos, pend)) {
             live = true;
             best = WOST_INF;
             bi = -1;
