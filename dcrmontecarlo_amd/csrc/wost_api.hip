@@ -407,8 +407,12 @@ int walk_mode(const wost_handle* h) {
 
 int ensure_tree(wost_handle* h) {
     if (h->tree_ready) return WOST_OK;
-    if (!build_segment_tree(h->nverts.data(), (int)(h->nverts.size() / 2), h->tree_leaf, &h->tree))
-        return fail(WOST_ERR_INVALID_ARG, "cannot build the Neumann segment tree");
+    const int nv = (int)(h->nverts.size() / 2);
+    // a polyline too long for kTreeMaxDepth levels at the chosen leaf size takes 32 per leaf
+    if (!build_segment_tree(h->nverts.data(), nv, h->tree_leaf, &h->tree) &&
+        !build_segment_tree(h->nverts.data(), nv, 32, &h->tree))
+        return fail(WOST_ERR_UNSUPPORTED, "cannot build the Neumann segment tree of %d segments (at most %d levels "
+                    "of 32-segment leaves)", nv - 1, kTreeMaxDepth);
     if (h->d_tree) (void)hipFree(h->d_tree);
     h->d_tree = nullptr;
     const size_t n = std::max<size_t>(h->tree.rec.size(), 16);

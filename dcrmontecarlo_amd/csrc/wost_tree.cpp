@@ -40,6 +40,7 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
     const int nleaves = (nseg + leaf - 1) / leaf;
     int D = 1, P = 4;                       // leaves at level D, P = 4^D leaf slots
     while (P < nleaves) { P *= 4; ++D; }
+    if (D > kTreeMaxDepth) return false;
     const int first_leaf = (P - 1) / 3;     // (4^D - 1) / 3 internal nodes
     const int n_nodes = first_leaf + P;
     out->first_leaf = first_leaf;

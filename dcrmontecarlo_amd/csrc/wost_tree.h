@@ -11,6 +11,9 @@ namespace wost {
 constexpr int kTreeChildFloats = 8;
 constexpr int kTreeArity = 4;
 constexpr int kTreeNodeFloats = kTreeArity * kTreeChildFloats;
+// the traversals keep 4 pending-child bits per level in 32 bits: at most 8 levels
+// below the root (4^8 leaves, 2^21 segments at 32 per leaf)
+constexpr int kTreeMaxDepth = 8;
 
 struct SegmentTreeHost {
     std::vector<float> rec;    // kTreeNodeFloats per internal node k: for child j = 0..3 (node 4k+1+j)
@@ -25,7 +28,8 @@ struct SegmentTreeHost {
 };
 
 // Builds the 4-ary tree of the polyline xy[2*nv] (nv >= 2) with `leaf` segments per
-// leaf (the leaf count padded to a power of 4). Returns false for a degenerate input.
+// leaf (the leaf count padded to a power of 4). Returns false for a degenerate input
+// or a tree deeper than kTreeMaxDepth.
 bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out);
 
 }  // namespace wost

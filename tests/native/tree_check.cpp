@@ -26,6 +26,13 @@ bool same(float a, float b) {
 
 extern "C" {
 
+// Depth of the tree built over xy[2 * nv] with `leaf` segments per leaf, or -1 when
+// build_segment_tree refuses it (degenerate input, deeper than kTreeMaxDepth).
+int tree_build_depth(const float* xy, int nv, int leaf) {
+    SegmentTreeHost th;
+    return build_segment_tree(xy, nv, leaf, &th) ? th.depth : -1;
+}
+
 // Node / leaf visits of the tree queries since the last call (4 counters).
 void tree_stats(long* out) {
 #if !defined(__HIP_DEVICE_COMPILE__)

@@ -39,6 +39,8 @@ def harness(tmp_path_factory):
     lib.tree_check_stop.argtypes = [fp, ctypes.c_int, ctypes.c_int, fp, fp, ctypes.c_float, ctypes.c_float,
                                     ctypes.c_long, ctypes.POINTER(ctypes.c_long)]
     lib.tree_check_stop.restype = ctypes.c_int
+    lib.tree_build_depth.argtypes = [fp, ctypes.c_int, ctypes.c_int]
+    lib.tree_build_depth.restype = ctypes.c_int
     return lib
 
 
@@ -228,3 +230,16 @@ def test_tree_nearest_crossing_matches_scan(harness, leaf):
     dirs[:k] = (zig[j] - pts[:k]).astype(np.float32)
     bad, hits = run_nearest(harness, zig.astype(np.float32), pts, dirs, radii, leaf)
     assert bad == 0 and hits > 1000
+
+
+def test_tree_depth_limit(harness):
+    """The traversals keep 4 pending-child bits per level in 32 bits (wost_tree.h
+    kTreeMaxDepth = 8): the builder refuses a deeper tree, and libwost then retries with
+    32-segment leaves (wost_api.hip ensure_tree) before failing loudly."""
+    n = 65536 + 2   # 65537 segments: 4^8 one-segment leaves are one too few
+    x = np.linspace(-1.0, 1.0, n, dtype=np.float32)
+    xy = np.ascontiguousarray(np.stack([x, np.sin(x)], 1), np.float32)
+    p = xy.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    assert harness.tree_build_depth(p, n - 1, 1) == 8     # 65535 segments
+    assert harness.tree_build_depth(p, n, 1) == -1        # 65537 segments
+    assert harness.tree_build_depth(p, n, 32) == 6
