@@ -523,7 +523,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     // waves per SIMD the register budget is sized for (tools/ab_bench.sh): 6, or 5 for the
     // cooperative tree kernels, whose record visits load four children's words at once
     // (profiles/r03_tree/tree_batch_waves_ab.log)
-    int waves = (tree && !mode_fix(mode)) ? 5 : 6;
+    int waves = tree ? 5 : 6;
     if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
     o << "extern \"C\" __global__ void __launch_bounds__(" << block << ", " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"

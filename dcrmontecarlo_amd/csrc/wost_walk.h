@@ -395,7 +395,9 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
 
 // intersect_polylines_tree<NORMAL> (wost_device.h, reference mode), the wave's lanes
 // sharing the search; `want`: this lane has a query.
-template <bool NORMAL = true>
+// NEAREST (compat="fixed"): the nearest crossing of intersect_polylines_tree<.., true>,
+// the lexicographic minimum of (t, segment), t > 0.
+template <bool NORMAL = true, bool NEAREST = false>
 __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, float px, float py, float dxi,
                                                              float dyi, float r, bool want, TreeWaveScratch* ws,
                                                              int lane) {
@@ -504,7 +506,25 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         }
         const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
-        if (live && s0 < s1) {
+        if (NEAREST && live && s0 < s1) {
+            float2 a = t.v[s0];
+            for (int i0 = s0; i0 < s1; i0 += 4) {   // vertices loaded four at a time
+                float2 bs[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) bs[u] = t.v[i0 + 1 + u <= nseg ? i0 + 1 + u : nseg];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (i0 + u < s1) {
+                        const int i = i0 + u;
+                        // t <= best (ties too: the lower segment index wins them)
+                        const float bq = best < WOST_INF ? bits_to_float(__builtin_bit_cast(int32_t, best) + 1) : best;
+                        const float tt = ray_segment_nearest_t(a, bs[u], qx, qy, ddx, ddy, bq);
+                        if (tt < best || (tt == best && i < bi)) { best = tt; bi = i; }
+                        a = bs[u];
+                    }
+                }
+            }
+        } else if (live && s0 < s1) {
             const float S = 2.0f * tol;
             const float m = fmaf(ddx, qy, -(ddy * qx));
             const float2 a = t.v[s0];
@@ -543,6 +563,7 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
     }
     const int wbi = key == ~0ull ? -1 : (int)(uint32_t)key;
     const float wbest = key == ~0ull ? WOST_INF : __builtin_bit_cast(float, (uint32_t)(key >> 32));
+    if (NEAREST) return ray_nearest_finish(wbi, wbest, px, py, dx, dy, qx0, qy0, r);
     return intersect_finish<NORMAL>(t.v, wbi, wbest, px, py, dx, dy, qx0, qy0, r);
 }
 
@@ -617,8 +638,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     lds += kStageN ? align16(sizeof(float2) * (size_t)A.nn) : 0;
     float* sPhi = reinterpret_cast<float*>(lds);
     lds += kStageN ? align16(sizeof(float) * (size_t)(A.nn > 1 ? A.nn - 1 : 0)) : 0;
-    // the cooperative tree queries (reference mode; compat="fixed" keeps the per-lane ones)
-    constexpr bool kWaveTree = TREE && !FIX;
+    // the cooperative tree queries (the silhouette and the step's ray query; compat="fixed"
+    // keeps the per-lane search for the source sample's visibility)
+    constexpr bool kWaveTree = TREE;
     TreeWaveScratch* const tws = reinterpret_cast<TreeWaveScratch*>(lds + 4 * sizeof(float4) * (size_t)A.tree_lds_records) +
                                  (threadIdx.x >> 6);
 
@@ -770,16 +792,17 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         if (!__any(active)) break;
         // a freshly refilled walk may already fail the while-condition (eps >= 1,
         // maxSteps == 0): it takes no step and is finished at the next iteration
-        const bool stepping = active && (k < A.max_steps) && (dD > A.eps);
+        bool stepping = active && (k < A.max_steps) && (dD > A.eps);
         // the cooperative tree queries need every lane of the wave: the others run the
         // step's pure arithmetic up to the ray query with them and leave after it
         if (kWaveTree ? !__any(stepping) : !stepping) continue;
 
         // --- one walk-step (:206-291)
         const float dd = fld.dirichlet_distance(dP, A.nd, px, py);  // :208
-        if (FIX && !(dd > A.eps)) {   // Q7/Q12 fixed: stop here, g at this point
+        if (FIX && stepping && !(dd > A.eps)) {   // Q7/Q12 fixed: stop here, g at this point
             dD = dd;
-            continue;
+            if (!kWaveTree) continue;
+            stepping = false;   // (it only helps the wave's tree queries)
         }
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
@@ -823,11 +846,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #if defined(WOST_ABL_NO_RAY)
             Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
 #else
-            const Hit h = FIX ? (TREE ? intersect_polylines_tree<false, true>(tree, px, py, cs, sn, r)
-                                      : fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r))
-                              : kWaveTree ? intersect_polylines_tree_wave<false>(tree, px, py, cs, sn, r, stepping, tws, lane)
-                              : TREE      ? intersect_polylines_tree<false>(tree, px, py, cs, sn, r)
-                                          : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
+            const Hit h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws, lane)
+                          : FIX       ? fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r)
+                                      : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
 #endif
             if (kWaveTree && !stepping) continue;   // the lanes that only helped
             xnx = h.x; xny = h.y; onB = h.hit;

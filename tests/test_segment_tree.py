@@ -199,6 +199,30 @@ def test_gpu_tree_walks_match_scan_walks(gpu_available):
         np.testing.assert_array_equal(v.view(np.uint32), ref[0].view(np.uint32), err_msg=str(key))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("knobs", [
+    {"WOST_TREE_LEAF": "1"}, {"WOST_TREE_LEAF": "32"},
+    {"WOST_JIT_TREE_SHARE": "0"}, {"WOST_JIT_TREE_SHARE": "64", "WOST_JIT_TREE_SHARE_MIN": "1"},
+    {"WOST_JIT_TREE_SHARE_DESCENT": "0", "WOST_JIT_TREE_BATCH": "1"},
+    {"WOST_JIT_TREE_BATCH": "2", "WOST_JIT_WAVES": "6"}])
+def test_gpu_cooperative_tree_variants_match_scan_walks(gpu_available, monkeypatch, knobs):
+    """The wave-cooperative tree queries (wost_walk.h: hand-outs of pending subtrees,
+    batched record loads) under every hand-out threshold, leaf size and load batch
+    give the scan kernel's walks bit for bit (the answers are order-independent
+    minima; only the visiting order and the lanes doing the visits change)."""
+    sc = S.wenner_topography(n_electrodes=16, n_walks=512, n_segments=2000)
+    s = sc.solver(device=0)
+    s.set_segment_tree(-1)
+    v0, st0 = s.solve_walks(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=21)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)   # read when the handle is created / the kernel is generated
+    s = sc.solver(device=0)
+    v1, st1 = s.solve_walks(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=21)
+    assert s.last_timing["tree"] == 1 and s.last_timing["jit"]
+    np.testing.assert_array_equal(st1, st0)
+    np.testing.assert_array_equal(v1.view(np.uint32), v0.view(np.uint32))
+
+
 def run_nearest(lib, verts, pts, dirs, radii, leaf=8):
     f = lambda a: np.ascontiguousarray(a, np.float32)
     verts, pts, dirs, radii = f(verts), f(pts), f(dirs), f(radii)
