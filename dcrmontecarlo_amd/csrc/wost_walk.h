@@ -300,10 +300,10 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
     };
     // hand out pending subtrees when few lanes still search (a uniform branch)
     auto share = [&](uint64_t L) {
-        if (!(__popcll(L) <= WOST_TREE_SHARE)) return;
+        if (!(__popcll(L) <= WOST_TREE_SHARE) || __ballot(live && pend != 0u) == 0ull) return;
         const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
         const PendCount pc = wave_pend_count(n);
-        if (pc.total < WOST_TREE_SHARE_MIN) return;
+        if (WOST_TREE_SHARE_MIN > 1 && pc.total < WOST_TREE_SHARE_MIN) return;
         // every lane leaves what it found in its owner's slot, then takes the owner's
         // best so far as its bound
         if (best < WOST_INF) atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
@@ -454,10 +454,10 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
                                             (unsigned long long)(uint32_t)bi);
     };
     auto share = [&](uint64_t L) {
-        if (!(__popcll(L) <= WOST_TREE_SHARE)) return;
+        if (!(__popcll(L) <= WOST_TREE_SHARE) || __ballot(live && pend != 0u) == 0ull) return;
         const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
         const PendCount pc = wave_pend_count(n);
-        if (pc.total < WOST_TREE_SHARE_MIN) return;
+        if (WOST_TREE_SHARE_MIN > 1 && pc.total < WOST_TREE_SHARE_MIN) return;
         deposit();
         if (tree_hand_out(ws, L, live, n, pc, lanes_below, owner, d, pos, pend)) {
             live = true;
@@ -694,10 +694,10 @@ __device__ __forceinline__ TreeStepAnswers tree_step_queries_wave(const SegTree&
     };
     // hand out pending subtrees of either kind when few lanes still search
     auto share = [&](uint64_t L) {
-        if (!(__popcll(L) <= WOST_TREE_SHARE)) return;
+        if (!(__popcll(L) <= WOST_TREE_SHARE) || __ballot(live && pend != 0u) == 0ull) return;
         const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
         const PendCount pc = wave_pend_count(n);
-        if (pc.total < WOST_TREE_SHARE_MIN) return;
+        if (WOST_TREE_SHARE_MIN > 1 && pc.total < WOST_TREE_SHARE_MIN) return;
         if (live && kind == 0 && best < WOST_INF)   // the owner's searches share their bound
             atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
         const uint64_t idle = ~L;
