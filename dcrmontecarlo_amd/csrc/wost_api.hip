@@ -378,11 +378,22 @@ float silhouette_stop2(float rmin) {
     return x;
 }
 
-// The segment tree's records are read through L1/L2 by 256-thread workgroups (LDS
-// staging of its top levels measured slower in round 2: profiles/r02_tree/ab_tree_lds.log).
-int tree_lds_records(const wost_handle*, int, int, int* block) {
+// Records of the segment tree staged in LDS by the field-specialised kernels: all of
+// them when they fit kTreeLdsMaxBytes (kTreeStageBlock-thread workgroups, two per CU),
+// else none (256-thread workgroups, records through L1/L2). WOST_TREE_LDS=0 disables
+// the staging (A/B; the results are the same bits either way).
+constexpr size_t kTreeLdsMaxBytes = 64 * 1024;
+int tree_lds_records(const wost_handle* h, int mode, int, int* block) {
     *block = kWalkBlock;
-    return 0;
+    if (!mode_tree(mode) || !h->tree_ready) return 0;
+    if (const char* e = std::getenv("WOST_TREE_LDS"))
+        if (std::atoi(e) == 0) return 0;
+    const int n = h->tree.first_leaf;
+    if (n <= 0 || (size_t)n * 8 * sizeof(float4) > kTreeLdsMaxBytes) return 0;
+    int b = kTreeStageBlock;
+    if (const char* e = std::getenv("WOST_TREE_LDS_BLOCK")) b = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
+    *block = b;
+    return n;
 }
 
 bool use_tree(const wost_handle* h) {
@@ -793,7 +804,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
     // polylines whose LDS copy would cost the walk kernel its occupancy are read from
     // global memory instead (field-specialised kernels; the precompiled ones stage them)
-    const bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds,
+    // (the staged tree records have their own budget, kTreeLdsMaxBytes)
+    const bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0,
                                                         jit_const_dirichlet(nd_)) > kGlobalPolylineLdsBytes;
     hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly);
     if (!jfn && block != kWalkBlock) {   // the precompiled kernels run 256-thread workgroups, no staged tree
@@ -804,13 +816,24 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
                     h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
     size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(nd_),
-                                jfn && jit_const_neumann(mode, nn_), jfn && gpoly);
+                                jfn && jit_const_neumann(mode, nn_), jfn && gpoly, block);
     // A/B knob (occupancy studies): WOST_LDS_PAD_BYTES extra bytes of LDS per workgroup
     if (const char* e = std::getenv("WOST_LDS_PAD_BYTES")) lds += (size_t)std::max(0, std::atoi(e));
     int blocks_per_cu = 0;
     if (jfn)
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
-    else
+    if (jfn && tree_lds > 0 && blocks_per_cu < 2) {
+        // the staged tree leaves room for fewer than two workgroups per CU: read the
+        // records through L1/L2 from 256-thread workgroups instead
+        block = kWalkBlock;
+        tree_lds = 0;
+        if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly)))
+            return fail(WOST_ERR_HIP, "field-specialised kernel unavailable: %s", h->jit_error.c_str());
+        lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0, jit_const_dirichlet(nd_), jit_const_neumann(mode, nn_),
+                             gpoly, block);
+        HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
+    }
+    if (!jfn)
         HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
                                &blocks_per_cu));
     if (blocks_per_cu < 1)

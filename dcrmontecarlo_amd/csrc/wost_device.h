@@ -1240,9 +1240,15 @@ struct SegTree {
     int depth;            // level of the leaves
     int leaf;             // segments per leaf
     float tol;            // line-test tolerance at the origin; grows with |q|
-    // word i (0..7) of internal node k's record, with a global load
+    const float4* lrec = nullptr;   // the first nlds records staged in LDS (walk kernels), or none
+    int nlds = 0;
+    // word i (0..7) of internal node k's record: an LDS read in the kernels that stage every
+    // record (WOST_TREE_STAGED, field-specialised kernels with kTreeStageBlock-thread
+    // workgroups), else a global load (a per-record choice would become a flat load)
     WOST_HD float4 word(int k, int i) const {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(WOST_TREE_STAGED)
+        return ((const __attribute__((address_space(3))) float4*)lrec)[8 * k + i];
+#elif defined(__HIP_DEVICE_COMPILE__)
         return ((const __attribute__((address_space(1))) float4*)rec)[8 * k + i];
 #else
         return rec[8 * k + i];

@@ -408,6 +408,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_TREE_SHARE " << std::max(0, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_DESCENT"))   // A/B: hand-outs during the descent
         o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
+    if (tree && block != kWalkBlock) o << "#define WOST_TREE_STAGED 1\n";   // every record in LDS
     if (const char* e = std::getenv("WOST_JIT_TREE_JOINT"))   // A/B: the two tree queries in one search
         o << "#define WOST_TREE_JOINT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_MIN"))   // A/B: fewest subtrees worth a hand-out
@@ -525,7 +526,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     // waves per SIMD the register budget is sized for (tools/ab_bench.sh): 6, or 5 for the
     // cooperative tree kernels, whose record visits load four children's words at once
     // (profiles/r03_tree/tree_batch_waves_ab.log)
-    int waves = tree ? 5 : 6;
+    // (4 when the tree's records are staged: two 8-wave workgroups per CU)
+    int waves = tree ? (block != kWalkBlock ? 4 : 5) : 6;
     if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
     o << "extern \"C\" __global__ void __launch_bounds__(" << block << ", " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"

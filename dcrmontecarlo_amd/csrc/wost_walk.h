@@ -48,7 +48,8 @@ struct WalkArgs {
     int32_t tree_leaf;
     float tree_tol;
     float tree_stop2;            // largest float whose sqrtf is <= rmin (< 0: none); silhouette_distance_tree
-    int32_t tree_lds_records;    // unused (0): the tree's records are read through L1/L2
+    int32_t tree_lds_records;    // records staged in LDS (the first ones, 128 B each; field-specialised
+                                 // kernels with kTreeStageBlock-thread workgroups), or 0: read through L1/L2
     int32_t tree_depth;          // level of the tree's leaves
     // walk-range batches (wost_solve_range): when range_walks > 0, local walk l is walk
     // range_offset + l % range_walks of point range_point0 + l / range_walks, i.e. global
@@ -80,6 +81,11 @@ __device__ __forceinline__ void point_alpha_body(const float2* pts, int64_t n, f
 }
 
 constexpr int kWalkBlock = 256;
+// workgroup of the field-specialised tree kernels that stage the tree's records in LDS:
+// 8 waves, two per SIMD, so two workgroups per CU place 4 waves on every SIMD (a
+// 640-thread workgroup places 3-3-2-2 and a second one no longer fits 5 per SIMD:
+// profiles/r03_tree/tree_lds_block_ab.log; WOST_TREE_LDS_BLOCK for A/B)
+constexpr int kTreeStageBlock = 512;
 
 // Walk recorder (solvers/WoStSolver.py:197-309, return_history). Record k < steps
 // of a walk is its step k: the pre-step point and its distances (:218-222), the
@@ -107,12 +113,13 @@ constexpr size_t kTreeWaveScratchBytes = sizeof(TreeWaveScratch);
 //  * the sampler's nodes 1..N-1 (node 0 is a kernel argument);
 //  * the Dirichlet vertices, unless the Fields policy has them compiled in;
 //  * the Neumann vertices and segment angles (scan kernels), unless compiled in;
-//  * with the segment tree, its first tree_lds records (64 B each), then one
-//    TreeWaveScratch per wave (the cooperative tree queries).
+//  * with the segment tree, its first tree_lds records (128 B each), then one
+//    TreeWaveScratch per wave (the cooperative tree queries) of the `block`-thread
+//    workgroup.
 // Query points are read from global memory (once per walk, at refill).
 WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false,
                                   bool delta = false, int tree_lds = 0, bool const_d = false, bool const_n = false,
-                                  bool global_polylines = false) {
+                                  bool global_polylines = false, int block = kWalkBlock) {
     if (global_polylines) const_d = const_n = true;   // nothing of the polylines is staged
     (void)n_points;
     size_t b = 0;
@@ -122,7 +129,8 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
     if (!const_d) b += align16(sizeof(float2) * (size_t)nd);
     if (neu && !tree && !const_n)
         b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
-    if (tree) b += 4 * sizeof(float4) * (size_t)tree_lds + kTreeWaveScratchBytes * (size_t)(kWalkBlock / 64);
+    if (tree)
+        b += 8 * sizeof(float4) * (size_t)tree_lds + kTreeWaveScratchBytes * (size_t)((block + 63) / 64);
     return b;
 }
 
@@ -968,8 +976,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #else
     constexpr bool kJoint = false;
 #endif
-    TreeWaveScratch* const tws = reinterpret_cast<TreeWaveScratch*>(lds + 4 * sizeof(float4) * (size_t)A.tree_lds_records) +
+    float4* const sRec = reinterpret_cast<float4*>(lds);   // staged tree records (TREE, tree_lds_records > 0)
+    const int n_rec = TREE ? A.tree_lds_records : 0;
+    TreeWaveScratch* const tws = reinterpret_cast<TreeWaveScratch*>(lds + 8 * sizeof(float4) * (size_t)n_rec) +
                                  (threadIdx.x >> 6);
+    for (int i = threadIdx.x; i < 8 * n_rec; i += blockDim.x) sRec[i] = A.tree[i];
 
     if (kStageD)
         for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
@@ -981,7 +992,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     const float2* const dP = GL ? A.dverts : sD;
     const float2* const nP = GL ? A.nverts : sN;
     const float* const phiP = GL ? A.seg_phi : sPhi;
-    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_depth, A.tree_leaf, A.tree_tol};
+    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_depth, A.tree_leaf, A.tree_tol, sRec, n_rec};
     float node0 = 0.0f;
     if (SRC) {
         node0 = A.table[0];
