@@ -101,9 +101,8 @@ WOST_HD size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 // LDS scratch of one wave for the cooperative tree queries (below): the hand-out
 // slots and one result slot per owner lane
 struct TreeWaveScratch {
-    uint32_t task[64];             // owner | level << 6 | position << 10 (joint: owner | kind << 6 | level << 7 | position << 11)
+    uint32_t task[64];             // owner | level << 6 | position << 10
     unsigned long long slot[64];   // silhouette: float bits of the squared distance; ray: s bits << 32 | segment
-    unsigned long long slot2[64];  // tree_step_queries_wave: the ray's slot (slot holds the silhouette's)
 };
 constexpr size_t kTreeWaveScratchBytes = sizeof(TreeWaveScratch);
 
@@ -157,9 +156,6 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 #endif
 #ifndef WOST_TREE_SHARE_DESCENT   // also at every level of the descent (else once per leaf round)
 #define WOST_TREE_SHARE_DESCENT 1
-#endif
-#ifndef WOST_TREE_JOINT   // the step's silhouette and ray queries in one cooperative search
-#define WOST_TREE_JOINT 0
 #endif
 #ifndef WOST_TREE_SHARE_MIN   // ... and at least this many subtrees are pending
 #define WOST_TREE_SHARE_MIN 1
@@ -579,323 +575,6 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
     return intersect_finish<NORMAL>(t.v, wbi, wbest, px, py, dx, dy, qx0, qy0, r);
 }
 
-// ---------------------------------------------------------------------------
-// Both tree queries of a step in one cooperative search (WOST_TREE_JOINT, off by
-// default: measured slower, 9.0e9 vs 1.04e10 on C5, profiles/r03_tree/joint_queries_ab.log).
-// The step's ray direction does not depend on r (only intersect_finish does), so
-// a lane whose silhouette search is over starts its own ray search at once, and
-// the wave's lanes hold tasks of either kind (silhouette or ray, for any owner).
-// Both kinds read the same 128-B records and leaf vertices, so a node visit or leaf
-// scan loads them before branching on the kind: the two dependent chains overlap
-// instead of adding. A task is a node to visit with a mask of children to test
-// (the silhouette's resume re-tests pending children of an ancestor: that is a
-// visit of the ancestor with the pending mask, in the same order as
-// silhouette_distance_tree's resume), or a leaf to scan. Same answers, bit for
-// bit: order-independent minima, as in the single-query functions above.
-// ---------------------------------------------------------------------------
-struct TreeStepAnswers {
-    float dn;              // silhouette distance (silhouette_distance_tree's contract)
-    int bi;                // the ray query's winning segment (-1: none)
-    float best;            // its s (reference) or t (NEAREST)
-    float dx, dy, qx, qy;  // unit direction, ray origin q = p + 1e-6 d
-    bool degenerate;       // |d| < 1e-10 (PolylinesSimple.py:151-156)
-};
-
-template <bool NEAREST>
-__device__ __forceinline__ TreeStepAnswers tree_step_queries_wave(const SegTree& t, float px, float py, float dd,
-                                                                  float stop2, float dxi, float dyi, bool want,
-                                                                  TreeWaveScratch* ws, int lane) {
-#pragma clang fp contract(off)
-    const uint64_t lanes_below = (1ull << lane) - 1ull;
-    const int nv = t.nv, nseg = nv - 1;
-    // this lane's own queries (helpers read them from its registers)
-    const float Town = (dd * dd) * 1.002f;
-    float dn_, dx, dy;
-    unit_direction(dxi, dyi, dn_, dx, dy);
-    const bool degenerate = dn_ < 1e-10f;
-    const float qx0 = px + 1e-6f * dx, qy0 = py + 1e-6f * dy;
-    ws->slot[lane] = (unsigned long long)__builtin_bit_cast(uint32_t, WOST_INF);
-    ws->slot2[lane] = ~0ull;
-    // the task: kind (0 silhouette, 1 ray), owner, node (d, pos) and the children to
-    // test there (cand), pending children of the ancestors (pend), its best so far
-    bool live = want && nv >= 3;
-    bool ray_todo = want && !degenerate && nv >= 2;   // the own ray query not started yet
-    int kind = 0, owner = lane, d = 0, pos = 0;
-    uint32_t cand = 15u, pend = 0u;
-    float best = WOST_INF;
-    int bi = -1;
-    float plb0 = WOST_INF, plb1 = WOST_INF, plb2 = WOST_INF, plb3 = WOST_INF, plb4 = WOST_INF;
-    // the task's query: silhouette (wx, wy) = p with bound wT; ray (wx, wy) = q, (wdx, wdy), wtol
-    float wx = px, wy = py, wT = Town, wdx = dx, wdy = dy, wtol = 0.0f;
-    auto plb_get = [&](int l) {
-        float v = -WOST_INF;
-        v = l == 0 ? plb0 : v; v = l == 1 ? plb1 : v; v = l == 2 ? plb2 : v;
-        v = l == 3 ? plb3 : v; v = l == 4 ? plb4 : v;
-        return v;
-    };
-    auto plb_set = [&](int l, float x) {
-        plb0 = l == 0 ? x : plb0; plb1 = l == 1 ? x : plb1; plb2 = l == 2 ? x : plb2;
-        plb3 = l == 3 ? x : plb3; plb4 = l == 4 ? x : plb4;
-    };
-    // the ray query of an owner whose direction is (ux, uy) and position (ox, oy): the
-    // same operations as intersect_polylines_tree, so the same bits on every lane
-    auto set_ray_query = [&](float ox, float oy, float ux, float uy) {
-        wdx = ux;
-        wdy = uy;
-        wx = ox + 1e-6f * ux;
-        wy = oy + 1e-6f * uy;
-        wtol = t.tol + 7.62939453125e-06f * (fabsf(wx) + fabsf(wy));   // + 2^-17 |q|_1
-    };
-    // a task's end: its minimum into the owner's slot
-    auto end_task = [&]() {
-        if (kind == 0) {
-            if (best < WOST_INF) atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
-        } else if (bi >= 0) {
-            atomicMin(&ws->slot2[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best + 0.0f) << 32 |
-                                             (unsigned long long)(uint32_t)bi);
-        }
-        live = false;
-        pend = 0u;
-    };
-    // no lane left its task yet: a lane without one takes its own ray query
-    auto start_own_ray = [&]() {
-        if (!live && ray_todo) {
-            ray_todo = false;
-            live = true;
-            kind = 1;
-            owner = lane;
-            d = 0;
-            pos = 0;
-            cand = 15u;
-            pend = 0u;
-            best = WOST_INF;
-            bi = -1;
-            set_ray_query(px, py, dx, dy);
-        }
-    };
-    // resume at the deepest pending children: the silhouette re-tests them with their
-    // parent's record (a visit of the ancestor with the pending mask), the ray takes
-    // the lowest one; false when nothing is pending
-    auto resume = [&]() {
-        if (kind == 0) {
-            while (pend != 0u) {
-                const int p = highest_bit(pend) >> 2;
-                const uint32_t m = (pend >> (4 * p)) & 15u;
-                pend &= ~(15u << (4 * p));
-                const float bound = best < wT ? best : wT;
-                if (plb_get(p) > bound) continue;
-                pos = pos >> (2 * (d - p));
-                d = p;
-                cand = m;
-                return true;
-            }
-            return false;
-        }
-        if (pend == 0u) return false;
-        const int p = highest_bit(pend) >> 2;
-        const int j = lowest_bit((pend >> (4 * p)) & 15u);
-        pend &= ~(1u << (4 * p + j));
-        pos = 4 * (pos >> (2 * (d - p))) + j;
-        d = p + 1;
-        cand = 15u;
-        return true;
-    };
-    // hand out pending subtrees of either kind when few lanes still search
-    auto share = [&](uint64_t L) {
-        if (!(__popcll(L) <= WOST_TREE_SHARE) || __ballot(live && pend != 0u) == 0ull) return;
-        const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
-        const PendCount pc = wave_pend_count(n);
-        if (WOST_TREE_SHARE_MIN > 1 && pc.total < WOST_TREE_SHARE_MIN) return;
-        if (live && kind == 0 && best < WOST_INF)   // the owner's searches share their bound
-            atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
-        const uint64_t idle = ~L;
-        const uint32_t nidle = (uint32_t)__popcll(idle);
-        uint32_t off = 0u;
-#pragma unroll
-        for (int b = 0; b < 5; ++b) off += (uint32_t)__popcll(pc.m[b] & lanes_below) << b;
-        if (live && off < nidle) {
-            const uint32_t give = n < nidle - off ? n : nidle - off;
-            for (uint32_t i = 0; i < give; ++i) {
-                const int b = lowest_bit(pend);
-                pend &= pend - 1u;
-                const int p = b >> 2, child = 4 * (pos >> (2 * (d - p))) + (b & 3);
-                ws->task[off + i] = (uint32_t)owner | (uint32_t)kind << 6 | (uint32_t)(p + 1) << 7 |
-                                    (uint32_t)child << 11;
-            }
-        }
-        wave_lds_sync();
-        const uint32_t rank = (uint32_t)__popcll(idle & lanes_below);
-        const bool helper = !live && rank < (pc.total < nidle ? pc.total : nidle);
-        if (helper) {
-            const uint32_t tk = ws->task[rank];
-            owner = (int)(tk & 63u);
-            kind = (int)((tk >> 6) & 1u);
-            d = (int)((tk >> 7) & 15u);
-            pos = (int)(tk >> 11);
-            cand = 15u;
-            pend = 0u;
-            best = WOST_INF;
-            bi = -1;
-            plb0 = plb1 = plb2 = plb3 = plb4 = WOST_INF;
-            live = true;
-        }
-        // the owners' queries (their own registers never change)
-        const float ox = __shfl(px, owner), oy = __shfl(py, owner), oT = __shfl(Town, owner);
-        const float ux = __shfl(dx, owner), uy = __shfl(dy, owner);
-        if (helper) {
-            if (kind == 0) { wx = ox; wy = oy; wT = oT; }
-            else set_ray_query(ox, oy, ux, uy);
-        }
-        if (live && kind == 0) {
-            const float sb = __builtin_bit_cast(float, (uint32_t)ws->slot[owner]);
-            best = sb < best ? sb : best;
-            if (best <= stop2) end_task();
-        }
-    };
-    wave_lds_sync();
-    start_own_ray();
-    for (;;) {
-        const uint64_t L = __ballot(live);
-        if (L == 0ull) break;
-        share(L);
-        // the descent, a uniform loop: every lane at a node visits it
-        for (;;) {
-            const bool down = live && d < t.depth;
-            if (!__any(down)) break;
-            if (down) {
-                const int k = tree_level_offset(d) + pos;
-                float4 w[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) w[i] = t.word(k, i);
-                uint32_t kept = 0u;
-                int nj = 0;
-                float nb2 = WOST_INF;
-                if (kind == 0) {
-                    const float bound = best < wT ? best : wT;
-                    float nb = WOST_INF;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        float lb;
-                        const bool kp = silhouette_child_keep(w[2 * j], w[2 * j + 1], wx, wy, bound, &lb);
-                        if (((cand >> j) & 1u) && kp) {
-                            kept |= 1u << j;
-                            if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
-                            else if (lb < nb2) nb2 = lb;
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float4 cu = w[2 * j], ab = w[2 * j + 1];
-                        bool kp = !(ab.x < 0.0f);
-                        const float cx = cu.x - wx, cy = cu.y - wy;
-                        const float cr = wdx * cu.w - wdy * cu.z, dt = wdx * cu.z + wdy * cu.w;
-                        kp = kp && !(fabsf(wdx * cy - wdy * cx) > (ab.x * fabsf(cr) + ab.y * fabsf(dt)) + wtol);
-#if !defined(WOST_NO_TREE_BEHIND)
-                        const float ahead = (wdx * cx + wdy * cy) + (ab.x * fabsf(dt) + ab.y * fabsf(cr));
-                        const bool front =
-                            !(ahead < -(512.0f * wtol + 1e-2f * ((fabsf(cx) + fabsf(cy)) + (ab.x + ab.y))));
-                        const bool parallel = !(ab.z * fabsf(cr) - ab.w * fabsf(dt) > 1e-3f);
-                        kp = kp && (ab.z == 3.0f || front || (!(ab.z == 2.0f) && parallel));
-#endif
-                        if (kp) kept |= 1u << j;
-                    }
-                    if (kept) nj = lowest_bit(kept);
-                }
-                if (kept) {
-                    pend |= (kept & ~(1u << nj)) << (4 * d);
-                    if (kind == 0) plb_set(d, nb2);
-                    pos = 4 * pos + nj;
-                    ++d;
-                    cand = 15u;
-                } else if (!resume()) {
-                    end_task();
-                }
-            }
-            start_own_ray();
-            share(__ballot(live));
-        }
-        // the leaves: vertices v[s0 .. s1 + 1] loaded four at a time whatever the kind
-        // (the silhouette reads the right neighbour's first segment too)
-        if (live) {
-            const int s0 = pos * t.leaf;
-            const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
-            const int j1 = s1 < nv - 2 ? s1 : nv - 2;
-            // the last vertex this kind reads (none: s0)
-            const int mend = kind == 0 ? (s0 + 1 <= j1 ? j1 + 1 : s0) : (s0 < s1 ? s1 : s0);
-            float2 va = t.v[s0 < nseg ? s0 : nseg];
-            float2 vb = va;
-            float cprev = 0.0f;
-            const float S = 2.0f * wtol;
-            const float mline = fmaf(wdx, wy, -(wdy * wx));
-            float ca = fmaf(wdx, va.y, -(wdy * va.x)) - mline;
-            uint32_t rc = 0u;
-            for (int m0 = s0 + 1; m0 <= mend; m0 += 4) {
-                float2 vv[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) vv[u] = t.v[m0 + u < nv ? m0 + u : nv - 1];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int m = m0 + u;
-                    if (m <= mend) {
-                        if (kind == 0) {
-                            if (m == s0 + 1) {
-                                vb = vv[u];
-                                cprev = (vb.x - va.x) * (wy - va.y) - (vb.y - va.y) * (wx - va.x);
-                            } else {   // vertex j = m - 1
-                                const float2 vc = vv[u];
-                                const float bpx = wx - vb.x, bpy = wy - vb.y;
-                                const float ccur = (vc.x - vb.x) * bpy - (vc.y - vb.y) * bpx;
-                                if (cprev * ccur < 0.0f) {
-                                    const float d2 = bpx * bpx + bpy * bpy;
-                                    best = d2 < best ? d2 : best;
-                                }
-                                cprev = ccur;
-                                vb = vc;
-                            }
-                        } else if (NEAREST) {   // segment i = m - 1
-                            const int i = m - 1;
-                            const float bq = best < WOST_INF ? bits_to_float(__builtin_bit_cast(int32_t, best) + 1) : best;
-                            const float tt = ray_segment_nearest_t(va, vv[u], wx, wy, wdx, wdy, bq);
-                            if (tt < best || (tt == best && i < bi)) { best = tt; bi = i; }
-                            va = vv[u];
-                        } else {   // segment m - 1: the per-vertex line filter
-                            const float cb = fmaf(wdx, vv[u].y, -(wdy * vv[u].x)) - mline;
-                            if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) rc |= 1u << (m - 1 - s0);
-                            ca = cb;
-                        }
-                    }
-                }
-            }
-            if (!NEAREST && kind == 1) {
-                while (rc != 0u) {
-                    const int i = s0 + lowest_bit(rc);
-                    rc &= rc - 1u;
-                    const float sv = ray_segment_time_filtered(t.v[i], t.v[i + 1], wx, wy, wdx, wdy);
-                    if (sv < best || (sv == best && i < bi)) { best = sv; bi = i; }
-                }
-            }
-            if (kind == 0 && best <= stop2) end_task();
-            else if (!resume()) end_task();
-        }
-        start_own_ray();
-    }
-    wave_lds_sync();
-    const float s2 = __builtin_bit_cast(float, (uint32_t)ws->slot[lane]);
-    const unsigned long long key = ws->slot2[lane];
-    wave_lds_sync();   // the slots are rewritten by the next query
-    TreeStepAnswers a;
-    a.dn = s2 == WOST_INF ? s2 : sqrt_rn(s2);
-    a.bi = key == ~0ull ? -1 : (int)(uint32_t)key;
-    a.best = key == ~0ull ? WOST_INF : __builtin_bit_cast(float, (uint32_t)(key >> 32));
-    a.dx = dx;
-    a.dy = dy;
-    a.qx = qx0;
-    a.qy = qy0;
-    a.degenerate = degenerate;
-    return a;
-}
-
 // The Fields policy F provides: has_g(), g(x,y), f(x,y), sigma(x,y),
 // alpha(x,y), alpha_jet(x,y), detached(), sigma_bar(), sqrt_sigma_bar(),
 // inv_sigma_bar(), and the polyline scans dirichlet_distance(sD,
@@ -970,12 +649,6 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     // the cooperative tree queries (the silhouette and the step's ray query; compat="fixed"
     // keeps the per-lane search for the source sample's visibility)
     constexpr bool kWaveTree = TREE;
-    // both queries in one search (tree_step_queries_wave); the ablations keep them apart
-#if WOST_TREE_JOINT && !defined(WOST_ABL_NO_SILHOUETTE) && !defined(WOST_ABL_NO_RAY)
-    constexpr bool kJoint = kWaveTree;
-#else
-    constexpr bool kJoint = false;
-#endif
     float4* const sRec = reinterpret_cast<float4*>(lds);   // staged tree records (TREE, tree_lds_records > 0)
     const int n_rec = TREE ? A.tree_lds_records : 0;
     TreeWaveScratch* const tws = reinterpret_cast<TreeWaveScratch*>(lds + 8 * sizeof(float4) * (size_t)n_rec) +
@@ -1142,9 +815,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             if (!kWaveTree) continue;
             stepping = false;   // (it only helps the wave's tree queries)
         }
-        // the step's random words and direction (:226-232); with the joint tree queries
-        // they are drawn before the silhouette query (the ray's direction does not
-        // depend on r), otherwise after it -- the same values either way
+        // the step's random words and direction (:226-232)
         U4 rn;
         float cs = 0.f, sn = 0.f;
         bool onB0 = false;                                           // the current point's, for FIX's
@@ -1171,20 +842,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             cs = f_cos(theta);                                       // :230-232
             sn = f_sin(theta);
         };
-        TreeStepAnswers ta;
-        if constexpr (kJoint) {   // both tree queries in one cooperative search
-            draw_direction();
-            ta = tree_step_queries_wave<FIX>(tree, px, py, dd, A.tree_stop2, cs, sn, stepping, tws, lane);
-            if (!stepping) continue;   // the lanes that only helped
-        }
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
         if (NEU) {
 #if defined(WOST_ABL_NO_SILHOUETTE)   // ablation (timing only)
             const float dn = TREE ? WOST_INF : fld.neumann_silhouette_distance(nP, A.nn, px, py);
 #else
-            const float dn = kJoint    ? ta.dn
-                           : kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane)
+            const float dn = kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane)
                            : TREE      ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
                                        : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
 #endif
@@ -1194,27 +858,16 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         } else {
             r = dd > A.rmin ? dd : A.rmin;                           // :215
         }
-        if constexpr (!kJoint) draw_direction();
+        draw_direction();
 
         float xnx, xny;
         if (NEU) {                                                   // :235-236
 #if defined(WOST_ABL_NO_RAY)
             Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
 #else
-            Hit h;
-            if constexpr (kJoint) {
-                if (ta.degenerate) {
-                    h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
-                } else if (FIX) {
-                    h = ray_nearest_finish(ta.bi, ta.best, px, py, ta.dx, ta.dy, ta.qx, ta.qy, r);
-                } else {
-                    h = intersect_finish<false>(tree.v, ta.bi, ta.best, px, py, ta.dx, ta.dy, ta.qx, ta.qy, r);
-                }
-            } else {
-                h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws, lane)
-                  : FIX       ? fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r)
-                              : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
-            }
+            const Hit h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws, lane)
+                          : FIX       ? fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r)
+                                      : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
 #endif
             if (kWaveTree && !stepping) continue;   // the lanes that only helped
             xnx = h.x; xny = h.y; onB = h.hit;

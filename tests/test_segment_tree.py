@@ -204,13 +204,13 @@ def test_gpu_tree_walks_match_scan_walks(gpu_available):
     {"WOST_TREE_LEAF": "1"}, {"WOST_TREE_LEAF": "32"},
     {"WOST_JIT_TREE_SHARE": "0"}, {"WOST_JIT_TREE_SHARE": "64", "WOST_JIT_TREE_SHARE_MIN": "1"},
     {"WOST_JIT_TREE_SHARE_DESCENT": "0", "WOST_JIT_TREE_BATCH": "1"},
-    {"WOST_JIT_TREE_BATCH": "2", "WOST_JIT_WAVES": "6"}, {"WOST_JIT_TREE_JOINT": "0"},
-    {"WOST_JIT_TREE_JOINT": "0", "WOST_JIT_TREE_SHARE": "0"}])
+    {"WOST_JIT_TREE_BATCH": "2", "WOST_JIT_WAVES": "6"}, {"WOST_TREE_LDS": "0"},
+    {"WOST_TREE_LDS": "0", "WOST_JIT_TREE_SHARE": "0"}])
 def test_gpu_cooperative_tree_variants_match_scan_walks(gpu_available, monkeypatch, knobs):
     """The wave-cooperative tree queries (wost_walk.h: hand-outs of pending subtrees,
-    batched record loads, the two queries of a step in one search or apart) under
-    every hand-out threshold, leaf size and load batch give the scan kernel's walks
-    bit for bit (the answers are order-independent
+    batched record loads, records staged in LDS or read through L1/L2) under every
+    hand-out threshold, leaf size and load batch give the scan kernel's walks bit
+    for bit (the answers are order-independent
     minima; only the visiting order and the lanes doing the visits change)."""
     sc = S.wenner_topography(n_electrodes=16, n_walks=512, n_segments=2000)
     s = sc.solver(device=0)
