@@ -257,8 +257,8 @@ int upload_program(wost_handle* h) {
 hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock,
                          bool global_polylines = false) {
     if (!h->jit_enabled) return nullptr;
-    const int key = (((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 2 + (block != kWalkBlock ? 1 : 0)) *
-                        2 + (global_polylines ? 1 : 0);
+    const int bk = block == kWalkBlock ? 0 : block == kTreeStageBlock ? 1 : block == kTreeStageVertsBlock ? 2 : 3;
+    const int key = (((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 4 + bk) * 2 + (global_polylines ? 1 : 0);
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
     h->jit_alpha_fn = nullptr;
@@ -378,18 +378,26 @@ float silhouette_stop2(float rmin) {
     return x;
 }
 
-// Records of the segment tree staged in LDS by the field-specialised kernels: all of
-// them when they fit kTreeLdsMaxBytes (kTreeStageBlock-thread workgroups, two per CU),
-// else none (256-thread workgroups, records through L1/L2). WOST_TREE_LDS=0 disables
-// the staging (A/B; the results are the same bits either way).
+// What of the segment tree the field-specialised kernels stage in LDS, by level:
+// 2 = its records and the Neumann vertices (one kTreeStageVertsBlock-thread workgroup
+// per CU), 1 = its records (two kTreeStageBlock-thread workgroups per CU), 0 = nothing
+// (256-thread workgroups, records and vertices through L1/L2). WOST_TREE_LDS caps the
+// level (A/B; the results are the same bits at every level). Returns the records to
+// stage and sets the workgroup size and the vertices to stage.
 constexpr size_t kTreeLdsMaxBytes = 64 * 1024;
-int tree_lds_records(const wost_handle* h, int mode, int, int* block) {
+constexpr int kTreeLdsDefaultLevel = 2;
+int tree_lds_records(const wost_handle* h, int mode, int level, int* block, int* verts) {
     *block = kWalkBlock;
+    *verts = 0;
     if (!mode_tree(mode) || !h->tree_ready) return 0;
-    if (const char* e = std::getenv("WOST_TREE_LDS"))
-        if (std::atoi(e) == 0) return 0;
+    if (const char* e = std::getenv("WOST_TREE_LDS")) level = std::min(level, std::max(0, std::atoi(e)));
     const int n = h->tree.first_leaf;
-    if (n <= 0 || (size_t)n * 8 * sizeof(float4) > kTreeLdsMaxBytes) return 0;
+    if (level <= 0 || n <= 0 || (size_t)n * 8 * sizeof(float4) > kTreeLdsMaxBytes) return 0;
+    if (level >= 2) {
+        *block = kTreeStageVertsBlock;
+        *verts = (int)(h->nverts.size() / 2);
+        return n;
+    }
     int b = kTreeStageBlock;
     if (const char* e = std::getenv("WOST_TREE_LDS_BLOCK")) b = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
     *block = b;
@@ -799,8 +807,9 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     } rec_free{d_rec};
     if (records) HIP_TRY(hipMalloc(&d_rec, (size_t)std::min<int64_t>(walks_total, batch_limit) * rec_walk_bytes));
 
-    int block = kWalkBlock;
-    int tree_lds = h->jit_enabled ? tree_lds_records(h, mode, (int)std::min<int64_t>(n_points, INT32_MAX), &block) : 0;
+    int block = kWalkBlock, tree_verts = 0;
+    int tree_level = kTreeLdsDefaultLevel;
+    int tree_lds = h->jit_enabled ? tree_lds_records(h, mode, tree_level, &block, &tree_verts) : 0;
     const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
     // polylines whose LDS copy would cost the walk kernel its occupancy are read from
     // global memory instead (field-specialised kernels; the precompiled ones stage them)
@@ -811,26 +820,27 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if (!jfn && block != kWalkBlock) {   // the precompiled kernels run 256-thread workgroups, no staged tree
         block = kWalkBlock;
         tree_lds = 0;
+        tree_verts = 0;
     }
     if (ns > 1 && !jfn)
         return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
                     h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
     size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(nd_),
-                                jfn && jit_const_neumann(mode, nn_), jfn && gpoly, block);
+                                jfn && jit_const_neumann(mode, nn_), jfn && gpoly, block, tree_verts);
     // A/B knob (occupancy studies): WOST_LDS_PAD_BYTES extra bytes of LDS per workgroup
     if (const char* e = std::getenv("WOST_LDS_PAD_BYTES")) lds += (size_t)std::max(0, std::atoi(e));
     int blocks_per_cu = 0;
     if (jfn)
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
-    if (jfn && tree_lds > 0 && blocks_per_cu < 2) {
-        // the staged tree leaves room for fewer than two workgroups per CU: read the
-        // records through L1/L2 from 256-thread workgroups instead
-        block = kWalkBlock;
-        tree_lds = 0;
+    while (jfn && tree_lds > 0 && blocks_per_cu * (block / 64) < 16) {
+        // what the tree stages leaves fewer than 16 waves per CU: stage less (the vertices,
+        // then the records), down to reading both through L1/L2 from 256-thread workgroups
+        tree_level = tree_verts > 0 ? 1 : 0;
+        tree_lds = tree_lds_records(h, mode, tree_level, &block, &tree_verts);
         if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly)))
             return fail(WOST_ERR_HIP, "field-specialised kernel unavailable: %s", h->jit_error.c_str());
-        lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0, jit_const_dirichlet(nd_), jit_const_neumann(mode, nn_),
-                             gpoly, block);
+        lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jit_const_dirichlet(nd_),
+                             jit_const_neumann(mode, nn_), gpoly, block, tree_verts);
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
     }
     if (!jfn)
@@ -867,6 +877,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_tol = h->tree.tol;
         a.tree_stop2 = silhouette_stop2(a.rmin);
         a.tree_lds_records = tree_lds;
+        a.tree_lds_verts = tree_verts;
         a.tree_depth = h->tree.depth;
     }
 

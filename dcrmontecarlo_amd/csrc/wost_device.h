@@ -1242,6 +1242,17 @@ struct SegTree {
     float tol;            // line-test tolerance at the origin; grows with |q|
     const float4* lrec = nullptr;   // the first nlds records staged in LDS (walk kernels), or none
     int nlds = 0;
+    const float2* lv = nullptr;     // the vertices staged in LDS (WOST_TREE_VSTAGED kernels), or none
+    // vertex i: an LDS read in the kernels that stage the vertices, else a global load
+    WOST_HD float2 vert(int i) const {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(WOST_TREE_VSTAGED)
+        return ((const __attribute__((address_space(3))) float2*)lv)[i];
+#elif defined(__HIP_DEVICE_COMPILE__)
+        return ((const __attribute__((address_space(1))) float2*)v)[i];
+#else
+        return v[i];
+#endif
+    }
     // word i (0..7) of internal node k's record: an LDS read in the kernels that stage every
     // record (WOST_TREE_STAGED, field-specialised kernels with kTreeStageBlock-thread
     // workgroups), else a global load (a per-record choice would become a flat load)
@@ -1427,11 +1438,11 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
         if (s0 + 1 <= j1) {
             // is_silhouette with each segment's cross product formed once (vertex j's
             // c2 is vertex j + 1's c1) and |b - x|^2 from x - b, as silhouette_distance
-            const float2 va = t.v[s0];
-            float2 vb = t.v[s0 + 1];
+            const float2 va = t.vert(s0);
+            float2 vb = t.vert(s0 + 1);
             float cprev = (vb.x - va.x) * (py - va.y) - (vb.y - va.y) * (px - va.x);
             for (int j = s0 + 1; j <= j1; ++j) {
-                const float2 vc = t.v[j + 1];
+                const float2 vc = t.vert(j + 1);
                 const float bpx = px - vb.x, bpy = py - vb.y;
                 const float ccur = (vc.x - vb.x) * bpy - (vc.y - vb.y) * bpx;
                 if (cprev * ccur < 0.0f) {
@@ -1529,9 +1540,9 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
         const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
         if (NEAREST && s0 < s1) {
-            float2 a = t.v[s0];
+            float2 a = t.vert(s0);
             for (int i = s0; i < s1; ++i) {
-                const float2 b = t.v[i + 1];
+                const float2 b = t.vert(i + 1);
                 // t <= best (ties too: the lower segment index wins them)
                 const float bq = best < WOST_INF ? bits_to_float(__builtin_bit_cast(int32_t, best) + 1) : best;   // t > 0
                 const float tt = ray_segment_nearest_t(a, b, qx, qy, dx, dy, bq);
@@ -1544,11 +1555,11 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
             // through the exact test; a leaf holds at most 32 segments
             const float S = 2.0f * tol;
             const float m = fmaf(dx, qy, -(dy * qx));
-            float2 a = t.v[s0];
+            float2 a = t.vert(s0);
             float ca = fmaf(dx, a.y, -(dy * a.x)) - m;
             uint32_t cand = 0u;
             for (int i = s0; i < s1; ++i) {
-                const float2 b = t.v[i + 1];
+                const float2 b = t.vert(i + 1);
                 const float cb = fmaf(dx, b.y, -(dy * b.x)) - m;
                 if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) cand |= 1u << (i - s0);
                 ca = cb;
@@ -1556,7 +1567,7 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
             while (cand != 0u) {
                 const int i = s0 + lowest_bit(cand);
                 cand &= cand - 1u;
-                const float s = ray_segment_time_filtered(t.v[i], t.v[i + 1], qx, qy, dx, dy);
+                const float s = ray_segment_time_filtered(t.vert(i), t.vert(i + 1), qx, qy, dx, dy);
                 if (s < best || (s == best && i < bi)) { best = s; bi = i; }
             }
         }

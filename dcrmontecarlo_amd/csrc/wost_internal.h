@@ -60,10 +60,11 @@ inline bool mode_delta(int m) {
 // kernels, wost_jit.cpp), so it stages no copy; a Neumann polyline is always staged
 // (const_n is kept for the callers).
 inline size_t walk_lds_bytes(int mode, int nd, int nn, int n_points, int tree_lds = 0, bool const_d = false,
-                             bool const_n = false, bool global_polylines = false, int block = kWalkBlock) {
+                             bool const_n = false, bool global_polylines = false, int block = kWalkBlock,
+                             int tree_verts = 0) {
     (void)const_n;   // the Neumann polyline is always staged (unless global_polylines)
     return walk_lds_bytes_for(mode_neu(mode), mode_src(mode), nd, nn, n_points, mode_tree(mode), mode_delta(mode),
-                              tree_lds, const_d, false, global_polylines, block);
+                              tree_lds, const_d, false, global_polylines, block, tree_verts);
 }
 // floats of the sampler / G_norm table buffer (WalkArgs::table); compat="fixed" delta
 // tracking appends the corrected screened sampler's [kFixRows][kFixCols] nodes

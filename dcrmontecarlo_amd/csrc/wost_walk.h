@@ -51,6 +51,8 @@ struct WalkArgs {
     int32_t tree_lds_records;    // records staged in LDS (the first ones, 128 B each; field-specialised
                                  // kernels with kTreeStageBlock-thread workgroups), or 0: read through L1/L2
     int32_t tree_depth;          // level of the tree's leaves
+    int32_t tree_lds_verts;      // Neumann vertices staged in LDS after the records (kTreeStageVertsBlock
+                                 // workgroups, WOST_TREE_VSTAGED kernels), or 0
     // walk-range batches (wost_solve_range): when range_walks > 0, local walk l is walk
     // range_offset + l % range_walks of point range_point0 + l / range_walks, i.e. global
     // id (range_point0 + l / range_walks) * walks_per_point + range_offset + l % range_walks
@@ -86,6 +88,8 @@ constexpr int kWalkBlock = 256;
 // 640-thread workgroup places 3-3-2-2 and a second one no longer fits 5 per SIMD:
 // profiles/r03_tree/tree_lds_block_ab.log; WOST_TREE_LDS_BLOCK for A/B)
 constexpr int kTreeStageBlock = 512;
+// ... and of those that stage the polyline's vertices as well: one 16-wave workgroup per CU
+constexpr int kTreeStageVertsBlock = 1024;
 
 // Walk recorder (solvers/WoStSolver.py:197-309, return_history). Record k < steps
 // of a walk is its step k: the pre-step point and its distances (:218-222), the
@@ -112,13 +116,13 @@ constexpr size_t kTreeWaveScratchBytes = sizeof(TreeWaveScratch);
 //  * the sampler's nodes 1..N-1 (node 0 is a kernel argument);
 //  * the Dirichlet vertices, unless the Fields policy has them compiled in;
 //  * the Neumann vertices and segment angles (scan kernels), unless compiled in;
-//  * with the segment tree, its first tree_lds records (128 B each), then one
-//    TreeWaveScratch per wave (the cooperative tree queries) of the `block`-thread
-//    workgroup.
+//  * with the segment tree, its first tree_lds records (128 B each), the tree_verts
+//    staged Neumann vertices, then one TreeWaveScratch per wave (the cooperative
+//    tree queries) of the `block`-thread workgroup.
 // Query points are read from global memory (once per walk, at refill).
 WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_points, bool tree = false,
                                   bool delta = false, int tree_lds = 0, bool const_d = false, bool const_n = false,
-                                  bool global_polylines = false, int block = kWalkBlock) {
+                                  bool global_polylines = false, int block = kWalkBlock, int tree_verts = 0) {
     if (global_polylines) const_d = const_n = true;   // nothing of the polylines is staged
     (void)n_points;
     size_t b = 0;
@@ -129,7 +133,8 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
     if (neu && !tree && !const_n)
         b += align16(sizeof(float2) * (size_t)nn) + align16(sizeof(float) * (size_t)(nn > 1 ? nn - 1 : 0));
     if (tree)
-        b += 8 * sizeof(float4) * (size_t)tree_lds + kTreeWaveScratchBytes * (size_t)((block + 63) / 64);
+        b += 8 * sizeof(float4) * (size_t)tree_lds + align16(sizeof(float2) * (size_t)tree_verts) +
+             kTreeWaveScratchBytes * (size_t)((block + 63) / 64);
     return b;
 }
 
@@ -361,14 +366,14 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
             const int j1 = s1 < nv - 2 ? s1 : nv - 2;
             bool stop = false;
             if (s0 + 1 <= j1) {
-                const float2 va = t.v[s0];
-                float2 vb = t.v[s0 + 1];
+                const float2 va = t.vert(s0);
+                float2 vb = t.vert(s0 + 1);
                 float cprev = (vb.x - va.x) * (qy - va.y) - (vb.y - va.y) * (qx - va.x);
                 // vertices loaded four at a time (indices clamped in range), then scanned
                 for (int j0 = s0 + 1; j0 <= j1; j0 += 4) {
                     float2 vcs[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) vcs[u] = t.v[j0 + 1 + u < nv ? j0 + 1 + u : nv - 1];
+                    for (int u = 0; u < 4; ++u) vcs[u] = t.vert(j0 + 1 + u < nv ? j0 + 1 + u : nv - 1);
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         if (j0 + u <= j1) {
@@ -515,11 +520,11 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
         if (NEAREST && live && s0 < s1) {
-            float2 a = t.v[s0];
+            float2 a = t.vert(s0);
             for (int i0 = s0; i0 < s1; i0 += 4) {   // vertices loaded four at a time
                 float2 bs[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) bs[u] = t.v[i0 + 1 + u <= nseg ? i0 + 1 + u : nseg];
+                for (int u = 0; u < 4; ++u) bs[u] = t.vert(i0 + 1 + u <= nseg ? i0 + 1 + u : nseg);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (i0 + u < s1) {
@@ -535,13 +540,13 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         } else if (live && s0 < s1) {
             const float S = 2.0f * tol;
             const float m = fmaf(ddx, qy, -(ddy * qx));
-            const float2 a = t.v[s0];
+            const float2 a = t.vert(s0);
             float ca = fmaf(ddx, a.y, -(ddy * a.x)) - m;
             uint32_t cand = 0u;
             for (int i0 = s0; i0 < s1; i0 += 4) {   // vertices loaded four at a time
                 float2 bs[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) bs[u] = t.v[i0 + 1 + u <= nseg ? i0 + 1 + u : nseg];
+                for (int u = 0; u < 4; ++u) bs[u] = t.vert(i0 + 1 + u <= nseg ? i0 + 1 + u : nseg);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (i0 + u < s1) {
@@ -554,7 +559,7 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
             while (cand != 0u) {
                 const int i = s0 + lowest_bit(cand);
                 cand &= cand - 1u;
-                const float s = ray_segment_time_filtered(t.v[i], t.v[i + 1], qx, qy, ddx, ddy);
+                const float s = ray_segment_time_filtered(t.vert(i), t.vert(i + 1), qx, qy, ddx, ddy);
                 if (s < best || (s == best && i < bi)) { best = s; bi = i; }
             }
         }
@@ -651,9 +656,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     constexpr bool kWaveTree = TREE;
     float4* const sRec = reinterpret_cast<float4*>(lds);   // staged tree records (TREE, tree_lds_records > 0)
     const int n_rec = TREE ? A.tree_lds_records : 0;
-    TreeWaveScratch* const tws = reinterpret_cast<TreeWaveScratch*>(lds + 8 * sizeof(float4) * (size_t)n_rec) +
-                                 (threadIdx.x >> 6);
+    lds += 8 * sizeof(float4) * (size_t)n_rec;
+    float2* const sVert = reinterpret_cast<float2*>(lds);  // staged Neumann vertices (TREE, tree_lds_verts > 0)
+    const int n_vert = TREE ? A.tree_lds_verts : 0;
+    lds += align16(sizeof(float2) * (size_t)n_vert);
+    TreeWaveScratch* const tws = reinterpret_cast<TreeWaveScratch*>(lds) + (threadIdx.x >> 6);
     for (int i = threadIdx.x; i < 8 * n_rec; i += blockDim.x) sRec[i] = A.tree[i];
+    for (int i = threadIdx.x; i < n_vert; i += blockDim.x) sVert[i] = A.nverts[i];
 
     if (kStageD)
         for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
@@ -665,7 +674,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     const float2* const dP = GL ? A.dverts : sD;
     const float2* const nP = GL ? A.nverts : sN;
     const float* const phiP = GL ? A.seg_phi : sPhi;
-    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_depth, A.tree_leaf, A.tree_tol, sRec, n_rec};
+    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_depth, A.tree_leaf, A.tree_tol, sRec, n_rec,
+                       sVert};
     float node0 = 0.0f;
     if (SRC) {
         node0 = A.table[0];
