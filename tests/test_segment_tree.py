@@ -204,7 +204,7 @@ def test_gpu_tree_walks_match_scan_walks(gpu_available):
     {"WOST_TREE_LEAF": "1"}, {"WOST_TREE_LEAF": "32"},
     {"WOST_JIT_TREE_SHARE": "0"}, {"WOST_JIT_TREE_SHARE": "64", "WOST_JIT_TREE_SHARE_MIN": "1"},
     {"WOST_JIT_TREE_SHARE_DESCENT": "0", "WOST_JIT_TREE_BATCH": "1"},
-    {"WOST_JIT_TREE_BATCH": "2", "WOST_JIT_WAVES": "6"}, {"WOST_TREE_LDS": "0"},
+    {"WOST_JIT_TREE_BATCH": "2", "WOST_JIT_WAVES": "6"}, {"WOST_TREE_LDS": "0"}, {"WOST_TREE_LDS": "1"},
     {"WOST_TREE_LDS": "0", "WOST_JIT_TREE_SHARE": "0"}])
 def test_gpu_cooperative_tree_variants_match_scan_walks(gpu_available, monkeypatch, knobs):
     """The wave-cooperative tree queries (wost_walk.h: hand-outs of pending subtrees,
@@ -223,6 +223,28 @@ def test_gpu_cooperative_tree_variants_match_scan_walks(gpu_available, monkeypat
     assert s.last_timing["tree"] == 1 and s.last_timing["jit"]
     np.testing.assert_array_equal(st1, st0)
     np.testing.assert_array_equal(v1.view(np.uint32), v0.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_segments,staged", [(10_000, True), (40_000, False)])
+def test_gpu_tree_lds_staging_levels(gpu_available, n_segments, staged):
+    """The field-specialised tree kernels stage the tree's records and the Neumann
+    vertices in LDS (one 1024-thread workgroup per CU) when they fit -- C5's 10k
+    segments do -- and step down to reading them through L1/L2 from 256-thread
+    workgroups when they do not (40k segments: 175 KB of records); either way the
+    walks are the scan kernel's, bit for bit."""
+    sc = S.wenner_topography(n_electrodes=8, n_walks=128, n_segments=n_segments)
+    res = []
+    for tree in (False, True):
+        s = sc.solver(device=0)
+        s.set_segment_tree(0 if tree else -1)
+        v, st = s.solve_walks(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=5)
+        assert s.last_timing["tree"] == int(tree)
+        res.append((v.ravel(), st.ravel(), s.last_timing["grid_blocks"]))
+    np.testing.assert_array_equal(res[1][1], res[0][1])
+    np.testing.assert_array_equal(res[1][0].view(np.uint32), res[0][0].view(np.uint32))
+    # 1,024 walks: one 1024-thread workgroup when staged, four 256-thread ones otherwise
+    assert res[1][2] == (1 if staged else 4), res[1][2]
 
 
 def run_nearest(lib, verts, pts, dirs, radii, leaf=8):
