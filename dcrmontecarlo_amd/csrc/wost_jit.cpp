@@ -44,7 +44,7 @@ namespace {
 // (intersect_polylines_compact) instead of the per-vertex line filter
 // (intersect_polylines_lines); 16384 the per-segment exact tests instead of either
 // two-pass scan for 8+ compiled-in segments; 32768 the one-pass compiled-in
-// silhouette scan instead of silhouette_distance_compact; ablation 65536 no tree
+// silhouette scan instead of silhouette_distance_compact; ablation 65536 no
 // silhouette query (dn = +inf).
 // Each bit only selects one fixed code path.
 int exp_flags() {

@@ -139,7 +139,9 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 }
 
 // ---------------------------------------------------------------------------
-// Wave-cooperative segment-tree queries (TREE kernels, reference mode).
+// Wave-cooperative segment-tree queries (TREE kernels; compat="fixed" too, its ray
+// query keyed by the nearest crossing's (t, segment)). The records and, when they
+// fit, the vertices are read from LDS (WOST_TREE_STAGED / WOST_TREE_VSTAGED kernels).
 //
 // silhouette_distance_tree / intersect_polylines_tree run one query per lane, and a
 // wave iterates until its slowest lane is done: at C5's walk positions ~89% of the
@@ -168,7 +170,6 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 #ifndef WOST_TREE_BATCH   // children of a record whose words are loaded together (1, 2 or 4)
 #define WOST_TREE_BATCH 4
 #endif
-
 
 // the LDS writes of the wave's lanes visible to its other lanes (a wave's LDS
 // operations complete in order; this keeps the compiler from moving them)
@@ -856,7 +857,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
         if (NEU) {
 #if defined(WOST_ABL_NO_SILHOUETTE)   // ablation (timing only)
-            const float dn = TREE ? WOST_INF : fld.neumann_silhouette_distance(nP, A.nn, px, py);
+            const float dn = WOST_INF;
 #else
             const float dn = kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane)
                            : TREE      ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
