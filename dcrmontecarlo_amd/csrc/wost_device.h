@@ -1138,13 +1138,20 @@ WOST_HD Hit intersect_polylines_lines(VP v, SP sv, float px, float py, float dxi
     const float qx = px + 1e-6f * dx, qy = py + 1e-6f * dy;
     const float m = fmaf(dx, qy, -(dy * qx));                              // cross(d, q)
     const float S = 7.62939453125e-06f * (c1 + (fabsf(qx) + fabsf(qy)));   // 2^-17
+    // a segment is a candidate unless both its endpoints lie beyond S on one side: two
+    // comparisons per vertex, shared by its two segments (the lanes' masks combine in
+    // scalar registers); a NaN distance makes its segments candidates (a superset,
+    // which the exact test then decides)
     uint64_t cand = 0ull;
-    float cprev = fmaf(dx, v[0].y, -(dy * v[0].x)) - m;
+    const float c0 = fmaf(dx, v[0].y, -(dy * v[0].x)) - m;
+    bool aprev = c0 > S, bprev = c0 < -S;
 #pragma unroll
     for (int i = 1; i < NV; ++i) {
         const float c = fmaf(dx, v[i].y, -(dy * v[i].x)) - m;              // cross(d, v_i - q) within its bound
-        if (fminf(cprev, c) <= S && fmaxf(cprev, c) >= -S) cand |= 1ull << (i - 1);
-        cprev = c;
+        const bool a = c > S, b = c < -S;
+        if (!((aprev && a) || (bprev && b))) cand |= 1ull << (i - 1);
+        aprev = a;
+        bprev = b;
     }
     float best = WOST_INF;
     int bi = -1;
@@ -1556,13 +1563,16 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
             const float S = 2.0f * tol;
             const float m = fmaf(dx, qy, -(dy * qx));
             float2 a = t.vert(s0);
-            float ca = fmaf(dx, a.y, -(dy * a.x)) - m;
+            const float ca = fmaf(dx, a.y, -(dy * a.x)) - m;
+            bool aprev = ca > S, bprev = ca < -S;   // the filter of intersect_polylines_lines
             uint32_t cand = 0u;
             for (int i = s0; i < s1; ++i) {
                 const float2 b = t.vert(i + 1);
                 const float cb = fmaf(dx, b.y, -(dy * b.x)) - m;
-                if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) cand |= 1u << (i - s0);
-                ca = cb;
+                const bool ab = cb > S, bb = cb < -S;
+                if (!((aprev && ab) || (bprev && bb))) cand |= 1u << (i - s0);
+                aprev = ab;
+                bprev = bb;
             }
             while (cand != 0u) {
                 const int i = s0 + lowest_bit(cand);

@@ -542,7 +542,8 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
             const float S = 2.0f * tol;
             const float m = fmaf(ddx, qy, -(ddy * qx));
             const float2 a = t.vert(s0);
-            float ca = fmaf(ddx, a.y, -(ddy * a.x)) - m;
+            const float ca = fmaf(ddx, a.y, -(ddy * a.x)) - m;
+            bool aprev = ca > S, bprev = ca < -S;   // the filter of intersect_polylines_lines
             uint32_t cand = 0u;
             for (int i0 = s0; i0 < s1; i0 += 4) {   // vertices loaded four at a time
                 float2 bs[4];
@@ -552,8 +553,10 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
                 for (int u = 0; u < 4; ++u) {
                     if (i0 + u < s1) {
                         const float cb = fmaf(ddx, bs[u].y, -(ddy * bs[u].x)) - m;
-                        if (fminf(ca, cb) <= S && fmaxf(ca, cb) >= -S) cand |= 1u << (i0 + u - s0);
-                        ca = cb;
+                        const bool ab = cb > S, bb = cb < -S;
+                        if (!((aprev && ab) || (bprev && bb))) cand |= 1u << (i0 + u - s0);
+                        aprev = ab;
+                        bprev = bb;
                     }
                 }
             }
