@@ -837,8 +837,15 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         // then the records), down to reading both through L1/L2 from 256-thread workgroups
         tree_level = tree_verts > 0 ? 1 : 0;
         tree_lds = tree_lds_records(h, mode, tree_level, &block, &tree_verts);
-        if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly)))
-            return fail(WOST_ERR_HIP, "field-specialised kernel unavailable: %s", h->jit_error.c_str());
+        if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly))) {
+            // the precompiled kernels then (256-thread workgroups, nothing of the tree staged)
+            block = kWalkBlock;
+            tree_lds = tree_verts = 0;
+            if (ns > 1)
+                return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel: %s",
+                            h->jit_error.c_str());
+            break;
+        }
         lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jit_const_dirichlet(nd_),
                              jit_const_neumann(mode, nn_), gpoly, block, tree_verts);
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
