@@ -883,6 +883,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_leaf = h->tree.leaf;
         a.tree_tol = h->tree.tol;
         a.tree_stop2 = silhouette_stop2(a.rmin);
+        a.tree_kmax = h->tree.kmax;
         a.tree_lds_records = tree_lds;
         a.tree_lds_verts = tree_verts;
         a.tree_depth = h->tree.depth;

@@ -1247,6 +1247,7 @@ struct SegTree {
     int depth;            // level of the leaves
     int leaf;             // segments per leaf
     float tol;            // line-test tolerance at the origin; grows with |q|
+    float kmax = 0.f;               // SegmentTreeHost::kmax (silhouette_child_keep_q)
     const float4* lrec = nullptr;   // the first nlds records staged in LDS (walk kernels), or none
     int nlds = 0;
     const float2* lv = nullptr;     // the vertices staged in LDS (WOST_TREE_VSTAGED kernels), or none
@@ -1344,6 +1345,30 @@ WOST_HD bool silhouette_child_keep(float4 cu, float4 ab, float px, float py, flo
     return !(ab.z * en - ab.w * (au + ab.x) > kConeMargin * (W + AB * 2.0f));
 }
 
+#ifndef WOST_TREE_QMARGIN   // the silhouette tests' rounding scales per query instead of per child
+#define WOST_TREE_QMARGIN 1
+#endif
+// silhouette_child_keep with the rounding scales taken per QUERY (WOST_TREE_QMARGIN):
+// sl and mc from Wq = 1.001 (|p|_1 + kmax) (SegmentTreeHost::kmax), which bounds every
+// child's W + a + b and W + 2 (a + b) above, their float rounding included -- a larger
+// slack only lowers the lower bound and a larger margin only keeps more children, so
+// the search stays exact; four fewer additions and two fewer products per child.
+WOST_HD bool silhouette_child_keep_q(float4 cu, float4 ab, float px, float py, float bound, float sl, float mc,
+                                     float* lb) {
+#pragma clang fp contract(off)
+    const float wx = px - cu.x, wy = py - cu.y;
+    const float pu = wx * cu.z + wy * cu.w, pn = wy * cu.z - wx * cu.w;
+    const float au = fabsf(pu), en = fabsf(pn) - ab.y;
+    float gu = (au - ab.x) - sl, gn = en - sl;
+    gu = gu > 0.0f ? gu : 0.0f;
+    gn = gn > 0.0f ? gn : 0.0f;
+    const float l = ab.x < 0.0f ? WOST_INF : (gu * gu + gn * gn) * 0.99999904632568359375f;   // 1 - 2^-20
+    *lb = l;
+    if (l > bound || ab.z == 2.0f) return false;
+    if (ab.z == 3.0f) return true;
+    return !(ab.z * en - ab.w * (au + ab.x) > mc);
+}
+
 // silhouette_distance for the use r = max(rmin, min(dn, dd)) of :210-212: exact
 // when the result is below dd and above rmin; otherwise some value >= dd (or
 // +inf), or some value <= rmin. stop2 is the largest float whose sqrtf is <= rmin
@@ -1364,6 +1389,10 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
     // levels: a level whose pending children all lie beyond the tightened bound is
     // dropped on resume without reloading its record (deeper levels are re-tested)
     float plb0 = WOST_INF, plb1 = WOST_INF, plb2 = WOST_INF, plb3 = WOST_INF, plb4 = WOST_INF;
+#if WOST_TREE_QMARGIN
+    const float qw = ((fabsf(px) + fabsf(py)) + t.kmax) * 1.001f;   // silhouette_child_keep_q
+    const float qsl = 9.5367431640625e-07f * qw, qmc = kConeMargin * qw;
+#endif
     auto plb_get = [&](int l) {
         float v = -WOST_INF;
         v = l == 0 ? plb0 : v; v = l == 1 ? plb1 : v; v = l == 2 ? plb2 : v;
@@ -1389,7 +1418,11 @@ WOST_HD float silhouette_distance_tree(const SegTree& t, float px, float py, flo
             if (!((cand >> j) & 1u)) continue;
             const float4 cu = t.word(k, 2 * j), ab = t.word(k, 2 * j + 1);
             float lb;
+#if WOST_TREE_QMARGIN
+            if (silhouette_child_keep_q(cu, ab, px, py, bound, qsl, qmc, &lb)) {
+#else
             if (silhouette_child_keep(cu, ab, px, py, bound, &lb)) {
+#endif
                 kept |= 1u << j;
                 if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
                 else if (lb < nb2) nb2 = lb;

@@ -410,6 +410,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
     if (tree && block != kWalkBlock) o << "#define WOST_TREE_STAGED 1\n";   // every record in LDS
     if (tree && block == kTreeStageVertsBlock) o << "#define WOST_TREE_VSTAGED 1\n";   // and the vertices
+    if (const char* e = std::getenv("WOST_JIT_TREE_QMARGIN"))   // A/B: per-query rounding scales
+        o << "#define WOST_TREE_QMARGIN " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_MIN"))   // A/B: fewest subtrees worth a hand-out
         o << "#define WOST_TREE_SHARE_MIN " << std::max(1, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_BATCH"))   // A/B: children loaded per batch

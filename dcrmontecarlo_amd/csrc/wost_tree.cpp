@@ -116,6 +116,13 @@ bool build_segment_tree(const float* xy, int nv, int leaf, SegmentTreeHost* out)
             o[7] = 0.f;
         }
     }
+    double kmax = 0.0;
+    for (int k = 1; k < n_nodes; ++k) {
+        const float* o = &node[(size_t)kTreeChildFloats * (size_t)k];
+        if (o[4] < 0.f) continue;
+        kmax = std::max(kmax, std::fabs((double)o[0]) + std::fabs((double)o[1]) + 2.0 * ((double)o[4] + o[5]));
+    }
+    out->kmax = (float)(kmax * (1.0 + std::ldexp(1.0, -10)));
     // child records of the internal nodes
     out->rec.assign((size_t)kTreeNodeFloats * (size_t)first_leaf, 0.f);
     for (int k = 0; k < first_leaf; ++k)

@@ -25,6 +25,8 @@ struct SegmentTreeHost {
     int depth = 0;             // level of the leaves (the root is level 0)
     int leaf = 0;              // segments per leaf
     float tol = 0.f;           // line-test tolerance at the origin; grows with |q|
+    float kmax = 0.f;          // max over the child boxes of |cx| + |cy| + 2 (a + b), rounded up: with
+                               // |p|_1 it bounds every per-child rounding scale of the silhouette tests
 };
 
 // Builds the 4-ary tree of the polyline xy[2*nv] (nv >= 2) with `leaf` segments per

@@ -48,6 +48,7 @@ struct WalkArgs {
     int32_t tree_leaf;
     float tree_tol;
     float tree_stop2;            // largest float whose sqrtf is <= rmin (< 0: none); silhouette_distance_tree
+    float tree_kmax;             // SegmentTreeHost::kmax
     int32_t tree_lds_records;    // records staged in LDS (the first ones, 128 B each; field-specialised
                                  // kernels with kTreeStageBlock-thread workgroups), or 0: read through L1/L2
     int32_t tree_depth;          // level of the tree's leaves
@@ -243,6 +244,9 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
     ws->slot[lane] = (unsigned long long)__builtin_bit_cast(uint32_t, WOST_INF);
     // the query this lane searches for (its own, or its owner's as a helper)
     float qx = px, qy = py, T = Town;
+    // its rounding scales (silhouette_child_keep_q, WOST_TREE_QMARGIN)
+    auto qscale = [&]() { return ((fabsf(qx) + fabsf(qy)) + t.kmax) * 1.001f; };
+    float qsl = 9.5367431640625e-07f * qscale(), qmc = kConeMargin * qscale();   // 2^-20 W, 1e-5 W
     int owner = lane;
     float best = WOST_INF;
     bool live = want && nv >= 3;
@@ -277,7 +281,11 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
             for (int u = 0; u < WOST_TREE_BATCH; ++u) {
                 const int j = j0 + u;
                 float lb;
+#if WOST_TREE_QMARGIN
+                const bool keep = silhouette_child_keep_q(w[2 * u], w[2 * u + 1], qx, qy, bound, qsl, qmc, &lb);
+#else
                 const bool keep = silhouette_child_keep(w[2 * u], w[2 * u + 1], qx, qy, bound, &lb);
+#endif
                 if (((cand >> j) & 1u) && keep) {
                     kept |= 1u << j;
                     if (lb < nb) { nb2 = nb; nb = lb; nj = j; }
@@ -325,6 +333,8 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
         qx = __shfl(px, owner);
         qy = __shfl(py, owner);
         T = __shfl(Town, owner);
+        qsl = 9.5367431640625e-07f * qscale();
+        qmc = kConeMargin * qscale();
         const float sb = __builtin_bit_cast(float, (uint32_t)ws->slot[owner]);
         best = sb < best ? sb : best;
         if (live && best <= stop2) { live = false; pend = 0u; }
@@ -678,8 +688,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     const float2* const dP = GL ? A.dverts : sD;
     const float2* const nP = GL ? A.nverts : sN;
     const float* const phiP = GL ? A.seg_phi : sPhi;
-    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_depth, A.tree_leaf, A.tree_tol, sRec, n_rec,
-                       sVert};
+    const SegTree tree{A.tree, A.nverts, A.nn, A.tree_first_leaf, A.tree_depth, A.tree_leaf, A.tree_tol, A.tree_kmax,
+                       sRec, n_rec, sVert};
     float node0 = 0.0f;
     if (SRC) {
         node0 = A.table[0];

@@ -52,7 +52,7 @@ int tree_check(const float* xy, int nv, int leaf, const float* pts, const float*
     SegmentTreeHost th;
     if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
     const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), reinterpret_cast<const float2*>(xy), nv,
-                    th.first_leaf, th.depth, th.leaf, th.tol};
+                    th.first_leaf, th.depth, th.leaf, th.tol, th.kmax};
     const float2* v = reinterpret_cast<const float2*>(xy);
     out[0] = out[1] = out[2] = out[3] = 0;
     for (long i = 0; i < n; ++i) {
@@ -81,7 +81,7 @@ int tree_check_stop(const float* xy, int nv, int leaf, const float* pts, const f
     SegmentTreeHost th;
     if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
     const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), reinterpret_cast<const float2*>(xy), nv,
-                    th.first_leaf, th.depth, th.leaf, th.tol};
+                    th.first_leaf, th.depth, th.leaf, th.tol, th.kmax};
     const float2* v = reinterpret_cast<const float2*>(xy);
     out[0] = out[1] = out[2] = 0;
 #if !defined(__HIP_DEVICE_COMPILE__)
@@ -110,7 +110,7 @@ int tree_check_nearest(const float* xy, int nv, int leaf, const float* pts, cons
     SegmentTreeHost th;
     if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
     const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), reinterpret_cast<const float2*>(xy), nv,
-                    th.first_leaf, th.depth, th.leaf, th.tol};
+                    th.first_leaf, th.depth, th.leaf, th.tol, th.kmax};
     const float2* v = reinterpret_cast<const float2*>(xy);
     out[0] = out[1] = 0;
     for (long i = 0; i < n; ++i) {

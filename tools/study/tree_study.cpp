@@ -24,7 +24,7 @@ int tree_counts(const float* xy, int nv, int leaf, const float* pts, const float
     SegmentTreeHost th;
     if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
     const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), reinterpret_cast<const float2*>(xy), nv,
-                    th.first_leaf, th.depth, th.leaf, th.tol};
+                    th.first_leaf, th.depth, th.leaf, th.tol, th.kmax};
     for (long i = 0; i < n; ++i) {
         for (int k = 0; k < 4; ++k) g_tree_stats[k] = 0;
         const float px = pts[2 * i], py = pts[2 * i + 1];
