@@ -357,6 +357,33 @@ def test_dcr_full_size_linearity(gpu_available):
     assert np.all(st1.mean_steps > 1)
 
 
+def test_variable_coefficients_full_size_homogeneity(gpu_available):
+    """C3 at its BASELINE size (configs[2]: 256 points x 100k walks, delta tracking and
+    the Neumann circle): the walks depend only on alpha and sigma, so doubling both the
+    boundary values g and the source f doubles every walk's total exactly (a power of
+    two): u(2g, 2f) must equal 2 u(g, f) bit for bit with identical step totals, and
+    the solve is deterministic."""
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd.geometry import PolyLinesSimple
+    from dcrmontecarlo_amd.solvers import WostSolver_2D
+
+    sc = S.variable_coefficients()
+    assert sc.points.shape[0] == 256 and sc.n_walks == 100_000
+    mk = lambda k: WostSolver_2D(PolyLinesSimple(sc.dirichlet), k * sc.g, PolyLinesSimple(sc.neumann),
+                                 source=k * sc.f, sigma=sc.sigma, alpha=sc.alpha)
+    s1, s2 = mk(1.0), mk(2.0)
+    assert s1.sigma_bar == s2.sigma_bar
+    kw = dict(nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=12, return_stats=True)
+    u1, st1 = s1.solve(sc.points, **kw)
+    u1b, st1b = s1.solve(sc.points, **kw)
+    u2, st2 = s2.solve(sc.points, **kw)
+    assert np.all(np.isfinite(st1.mean))
+    assert np.array_equal(st1.mean, st1b.mean) and st1.total_steps == st1b.total_steps
+    assert np.array_equal(st2.mean, 2.0 * st1.mean)
+    assert st1.total_steps == st2.total_steps
+    assert st1.total_steps > 256 * 100_000 * 10
+
+
 # ---------------------------------------------------------------- edge cases
 def test_edge_cases(gpu_available):
     from dcrmontecarlo_amd import fields as F
