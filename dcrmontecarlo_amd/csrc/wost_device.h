@@ -1141,14 +1141,18 @@ WOST_HD Hit intersect_polylines_lines(VP v, SP sv, float px, float py, float dxi
     // a segment is a candidate unless both its endpoints lie beyond S on one side: two
     // comparisons per vertex, shared by its two segments (the lanes' masks combine in
     // scalar registers); a NaN distance makes its segments candidates (a superset,
-    // which the exact test then decides)
+    // which the exact test then decides). cross(d, v_i) is compared with m +- S
+    // rounded once, not cross(d, v_i) - m with +-S: that moves the threshold by at
+    // most 2^-23 (|v_i|_1 + |q|_1), 1/64 of S, inside the margin, and saves a
+    // subtraction per vertex
+    const float hi = m + S, lo = m - S;
     uint64_t cand = 0ull;
-    const float c0 = fmaf(dx, v[0].y, -(dy * v[0].x)) - m;
-    bool aprev = c0 > S, bprev = c0 < -S;
+    const float c0 = fmaf(dx, v[0].y, -(dy * v[0].x));
+    bool aprev = c0 > hi, bprev = c0 < lo;
 #pragma unroll
     for (int i = 1; i < NV; ++i) {
-        const float c = fmaf(dx, v[i].y, -(dy * v[i].x)) - m;              // cross(d, v_i - q) within its bound
-        const bool a = c > S, b = c < -S;
+        const float c = fmaf(dx, v[i].y, -(dy * v[i].x));                  // cross(d, v_i) within its bound
+        const bool a = c > hi, b = c < lo;
         if (!((aprev && a) || (bprev && b))) cand |= 1ull << (i - 1);
         aprev = a;
         bprev = b;
@@ -1595,14 +1599,15 @@ WOST_HD Hit intersect_polylines_tree(const SegTree& t, float px, float py, float
             // through the exact test; a leaf holds at most 32 segments
             const float S = 2.0f * tol;
             const float m = fmaf(dx, qy, -(dy * qx));
+            const float hi = m + S, lo = m - S;   // the thresholds of intersect_polylines_lines
             float2 a = t.vert(s0);
-            const float ca = fmaf(dx, a.y, -(dy * a.x)) - m;
-            bool aprev = ca > S, bprev = ca < -S;   // the filter of intersect_polylines_lines
+            const float ca = fmaf(dx, a.y, -(dy * a.x));
+            bool aprev = ca > hi, bprev = ca < lo;   // the filter of intersect_polylines_lines
             uint32_t cand = 0u;
             for (int i = s0; i < s1; ++i) {
                 const float2 b = t.vert(i + 1);
-                const float cb = fmaf(dx, b.y, -(dy * b.x)) - m;
-                const bool ab = cb > S, bb = cb < -S;
+                const float cb = fmaf(dx, b.y, -(dy * b.x));
+                const bool ab = cb > hi, bb = cb < lo;
                 if (!((aprev && ab) || (bprev && bb))) cand |= 1u << (i - s0);
                 aprev = ab;
                 bprev = bb;

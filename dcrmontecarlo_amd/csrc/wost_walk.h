@@ -551,9 +551,10 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         } else if (live && s0 < s1) {
             const float S = 2.0f * tol;
             const float m = fmaf(ddx, qy, -(ddy * qx));
+            const float hi = m + S, lo = m - S;     // the thresholds of intersect_polylines_lines
             const float2 a = t.vert(s0);
-            const float ca = fmaf(ddx, a.y, -(ddy * a.x)) - m;
-            bool aprev = ca > S, bprev = ca < -S;   // the filter of intersect_polylines_lines
+            const float ca = fmaf(ddx, a.y, -(ddy * a.x));
+            bool aprev = ca > hi, bprev = ca < lo;   // the filter of intersect_polylines_lines
             uint32_t cand = 0u;
             for (int i0 = s0; i0 < s1; i0 += 4) {   // vertices loaded four at a time
                 float2 bs[4];
@@ -562,8 +563,8 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (i0 + u < s1) {
-                        const float cb = fmaf(ddx, bs[u].y, -(ddy * bs[u].x)) - m;
-                        const bool ab = cb > S, bb = cb < -S;
+                        const float cb = fmaf(ddx, bs[u].y, -(ddy * bs[u].x));
+                        const bool ab = cb > hi, bb = cb < lo;
                         if (!((aprev && ab) || (bprev && bb))) cand |= 1u << (i0 + u - s0);
                         aprev = ab;
                         bprev = bb;
