@@ -14,22 +14,25 @@ are all-gathered over xGMI (the only data-path collective) and summed per
 electrode in global block order -- bitwise a one-GPU solve of W walks per
 electrode. --scaling weak (default): W = N x 1M, so each GPU keeps the one-GPU
 workload; --scaling strong: W = 1M split N ways. The communicator's id travels
-through the launcher's TCP store; no torch process group is created.
+through a standard-library socket store hosted by rank 0 (comm.launch_store); no
+torch process group is created.
 
 --workload wenner_topography (BASELINE configs[4]): the 256-electrode
 Wenner-alpha line over the 10,000-segment topography, model and homogeneous
 background, every electrode's walks scoring the (<= 16) transmitters it receives
 (survey.run_wenner_survey); one bench step = one whole survey. N ranks shard every
-group's walks by walk range (comm.solve_sources_distributed, one communicator per
-field so the two fields run concurrently); weak scaling keeps --walks per electrode
-per GPU. Its cpu_baseline is the oracle's brute-force scan (the reference's
+group's walks by walk range over ONE communicator (survey._run_fields_distributed: the
+model and background fields' local solves run concurrently, one thread issues every
+collective in a fixed order); weak scaling keeps --walks per electrode per GPU. Its cpu_baseline is the oracle's brute-force scan (the reference's
 algorithm), and the segment tree's gain is reported as speedup_vs_bruteforce
 against the device's own brute-force scan kernel (never as a roofline
 fraction).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
-                       [--workload dcr_dipole|wenner_topography]
-       (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+                       [--workload dcr_dipole|wenner_topography|variable_coefficients]
+       --gpus N > 1 starts N rank processes itself (launch_ranks; the parent makes no HIP
+       call); under a launcher (python -m torch.distributed.run --nproc-per-node N
+       bench.py --gpus N ...) WORLD_SIZE must equal --gpus.
 Prints one JSON line on rank 0.
 """
 from __future__ import annotations
@@ -65,6 +68,9 @@ def parse():
                     help="weak: N x --walks walks per electrode on N GPUs (default); strong: --walks on N GPUs")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-rho", action="store_true", help="skip the apparent-resistivity leg (profiling runs)")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="only launch the ranks: each prints its RANK/LOCAL_RANK/WORLD_SIZE as JSON (no GPU)")
+    ap.add_argument("--dry-launch-fail-rank", type=int, default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -256,11 +262,102 @@ def issue_line(perfmodel, kernel_steps_per_s: float):
     return out
 
 
-def main():
-    args = parse()
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """bench.py --gpus N (N > 1) without a launcher: start N rank processes of this script
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR = 127.0.0.1 and a free MASTER_PORT,
+    where rank 0 hosts the communicator's id store) and wait for them. This parent makes
+    no HIP call (it imports nothing of the package). When a rank fails, the others are
+    stopped (they would wait for it in the id exchange or RCCL) and its exit code is
+    returned; 0 when every rank succeeded."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WOST_BENCH_LAUNCHED="1")
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    def stop(ranks):
+        for q in ranks:
+            procs[q].send_signal(signal.SIGTERM)
+        t0 = time.time()
+        for q in ranks:
+            try:
+                procs[q].wait(timeout=max(0.1, 20.0 - (time.time() - t0)))
+            except subprocess.TimeoutExpired:
+                procs[q].kill()
+                procs[q].wait()
+
+    live = set(range(n))
+    try:
+        while live:
+            failed = None
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is not None:
+                    live.discard(r)
+                    if code != 0:
+                        failed = (r, code)
+                        break
+            if failed is not None:
+                r, code = failed
+                print(f"bench.py: rank {r} exited with status {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop(sorted(live))
+                return code if code > 0 else 128 - code     # killed by signal s: 128 + s
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        stop(sorted(live))
+        raise
+    return 0
+
+
+def check_launch(args) -> tuple[int, int, int]:
+    """(world, rank, local rank) of this process. Under a launcher (WORLD_SIZE set) --gpus
+    must equal WORLD_SIZE; a rank whose LOCAL_RANK device does not exist exits non-zero."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.dry_launch:
+        return world, rank, local
+    from dcrmontecarlo_amd import _lib
+
+    ndev = _lib.device_count()
+    if local >= ndev:
+        sys.exit(f"bench.py: rank {rank} needs device {local} (LOCAL_RANK) but this node has {ndev} visible "
+                 f"GPU(s); run with --gpus <= {ndev}")
+    return world, rank, local
+
+
+def main():
+    args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world, rank, local = check_launch(args)
+    if args.dry_launch:
+        # the launch alone (CPU tests): report this rank's environment, fail on request
+        print(json.dumps({"rank": rank, "local_rank": local, "world_size": world,
+                          "master_addr": os.environ.get("MASTER_ADDR"), "master_port": os.environ.get("MASTER_PORT"),
+                          "pid": os.getpid(), "ppid": os.getppid()}), flush=True)
+        if args.dry_launch_fail_rank == rank:
+            sys.exit(3)
+        if args.dry_launch_fail_rank is not None:
+            time.sleep(30)   # the healthy ranks: the launcher must stop them
+        return
     if args.workload == "wenner_topography":
         return wenner_main(args, world, rank, local)
     args.walks = args.walks or 1_000_000
@@ -459,20 +556,18 @@ def wenner_main(args, world, rank, local):
     sc = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=args.fields == "physical")
     sm = sc.solver(device=local)
     sh = survey.homogeneous_solver(sc, WENNER_ALPHA_BG, sm, device=local)
-    comms = None
+    comm = None
     if world > 1 or os.environ.get("WOST_BENCH_FORCE_COMM"):
-        cm = C.Communicator.from_env(device=local)
-        ch = C.Communicator.from_env(device=local, key="wost_comm_uid_background", store=getattr(cm, "_store", None))
-        comms = (cm, ch)
+        comm = C.Communicator.from_env(device=local)
     Wt = W1 * (world if args.scaling == "weak" else 1)
     w0, w1 = C.shard_walk_range(Wt, world, rank)
 
     def step(seed, walks=Wt):
-        return survey.run_wenner_survey(sc, WENNER_ALPHA_BG, walks, seed=seed, solvers=(sm, sh), comm=comms)
+        return survey.run_wenner_survey(sc, WENNER_ALPHA_BG, walks, seed=seed, solvers=(sm, sh), comm=comm)
 
     def barrier():
-        if comms is not None:
-            comms[0].barrier()
+        if comm is not None:
+            comm.barrier()
 
     for k in range(args.warmup):
         step(1000 + k)
@@ -486,13 +581,13 @@ def wenner_main(args, world, rank, local):
         kernel_ms += float(res.kernel_ms)          # this rank's walk-kernel time, both fields
     barrier()
     elapsed = time.perf_counter() - t0
-    max_elapsed = elapsed if comms is None else float(comms[0].allreduce([elapsed], "max")[0])
+    max_elapsed = elapsed if comm is None else float(comm.allreduce([elapsed], "max")[0])
     res_phys = None
     if args.fields == "literal":   # outside the timed region: the physical survey's rho_a
         sp = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=True)
         pm = sp.solver(device=local)
         ph = survey.homogeneous_solver(sp, WENNER_ALPHA_BG, pm, device=local)
-        res_phys = survey.run_wenner_survey(sp, WENNER_ALPHA_BG, Wt, seed=4242, solvers=(pm, ph), comm=comms)
+        res_phys = survey.run_wenner_survey(sp, WENNER_ALPHA_BG, Wt, seed=4242, solvers=(pm, ph), comm=comm)
 
     if rank == 0:
         value = steps_all / max_elapsed
@@ -510,8 +605,8 @@ def wenner_main(args, world, rank, local):
                        "walks_per_electrode": Wt, "walks_per_electrode_per_gpu": w1 - w0,
                        "launches_per_field": res.launches, "walk_steps_per_survey": steps_all // max(args.steps, 1),
                        "parallelism": (f"walk-range shards of every electrode over {world} GPUs "
-                                       "(comm.solve_sources_distributed: libwost RCCL all-gather of block sums, "
-                                       "one communicator per field)") if world > 1 else "one GPU"},
+                                       "(libwost's protocol over its RCCL communicator, all-gather of block sums; "
+                                       "both fields' collectives in a fixed order)") if world > 1 else "one GPU"},
             # walk-steps over the walk kernels' summed times: the model and background fields
             # run concurrently, so this understates the kernel rate
             "survey_kernel_walk_steps_per_s_fields_summed": kernel_rate,
@@ -571,10 +666,9 @@ def wenner_main(args, world, rank, local):
                                                  "their rho_a is not physical)")
             out["rho_a_literal_timed_survey"] = rho_summary(res, sc.name)
         print(json.dumps(out), flush=True)
-    if comms is not None:
-        comms[0].barrier()
-        for c in comms:
-            c.close()
+    if comm is not None:
+        comm.barrier()
+        comm.close()
 
 
 if __name__ == "__main__":

@@ -8,19 +8,196 @@ global block order: the result is bitwise that of a one-GPU solve for any R
 (SURVEY.md 8e). The reference has no parallel code.
 
 The only thing libwost needs from outside is the 128-byte RCCL unique id, made on one
-rank and handed to the others: ``Communicator.from_env`` uses the launcher's TCP
-store (torchrun's MASTER_ADDR/MASTER_PORT; no process group), ``from_torch`` an
-initialised torch.distributed group, ``from_file`` a file every rank can read.
+rank and handed to the others. ``Communicator.from_env`` does it without PyTorch: rank 0
+hosts a small key-value store on MASTER_ADDR:MASTER_PORT (:class:`SocketStore`, the
+standard library's sockets); under torchrun, whose elastic agent already listens on
+MASTER_PORT, the ranks of one node meet in a file named after their common parent (the
+agent) instead, and only a multi-node torchrun job uses torch's TCPStore client.
+``from_torch`` takes an initialised torch.distributed group, ``from_file`` a file every
+rank can read.
 """
 from __future__ import annotations
 
 import ctypes
 import os
+import socket
+import socketserver
+import struct
+import tempfile
+import threading
 import time
 
 import numpy as np
 
 from . import _lib
+
+
+class _StoreHandler(socketserver.StreamRequestHandler):
+    """One client connection: requests b"S" key value (set) and b"G" key (get, waits
+    until the key is set); keys and values are length-prefixed (u32, big endian)."""
+
+    def _read(self):
+        n = struct.unpack(">I", self.rfile.read(4))[0]
+        return self.rfile.read(n)
+
+    def handle(self):
+        try:
+            self._serve()
+        except (OSError, struct.error):   # a client that went away mid-request
+            return
+
+    def _serve(self):
+        st = self.server.store
+        while True:
+            op = self.rfile.read(1)
+            if not op:
+                return
+            key = self._read()
+            if op == b"S":
+                val = self._read()
+                with st.cond:
+                    st.kv[key] = val
+                    st.cond.notify_all()
+                self.wfile.write(b"\x00")
+            elif op == b"G":
+                with st.cond:
+                    ok = st.cond.wait_for(lambda: key in st.kv or st.closed, timeout=st.timeout)
+                    val = st.kv.get(key) if ok else None
+                if val is None:
+                    self.wfile.write(b"\x01")
+                    return
+                self.wfile.write(b"\x00" + struct.pack(">I", len(val)) + val)
+            else:
+                return
+
+
+class _StoreServer(socketserver.ThreadingTCPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+
+
+class SocketStore:
+    """A minimal key-value store over TCP (standard library only) for the communicator's
+    id: rank 0 hosts it (``is_master``), every rank -- rank 0 too -- is a client. ``get``
+    blocks until the key is set or ``timeout`` passes. The host keeps serving until
+    ``close`` (the communicator holds its store for its lifetime)."""
+
+    def __init__(self, host: str, port: int, is_master: bool, timeout: float = 300.0):
+        self.timeout = float(timeout)
+        self._srv = None
+        if is_master:
+            self.kv, self.cond, self.closed = {}, threading.Condition(), False
+            self._srv = _StoreServer(("", int(port)), _StoreHandler)
+            self._srv.store = self
+            threading.Thread(target=self._srv.serve_forever, daemon=True).start()
+        t0 = time.time()
+        while True:   # the host may not listen yet
+            try:
+                self._sock = socket.create_connection((host, int(port)), timeout=self.timeout)
+                break
+            except OSError:
+                if time.time() - t0 > self.timeout:
+                    raise TimeoutError(f"no store at {host}:{port} after {self.timeout} s") from None
+                time.sleep(0.05)
+        self._sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self._f = self._sock.makefile("rwb")
+
+    @staticmethod
+    def _lp(b: bytes) -> bytes:
+        return struct.pack(">I", len(b)) + b
+
+    def set(self, key: str, value: bytes):
+        self._f.write(b"S" + self._lp(key.encode()) + self._lp(bytes(value)))
+        self._f.flush()
+        if self._f.read(1) != b"\x00":
+            raise ConnectionError("store: set failed")
+
+    def get(self, key: str) -> bytes:
+        self._f.write(b"G" + self._lp(key.encode()))
+        self._f.flush()
+        st = self._f.read(1)
+        if st != b"\x00":
+            raise TimeoutError(f"store: no value for {key!r} within {self.timeout} s")
+        n = struct.unpack(">I", self._f.read(4))[0]
+        return self._f.read(n)
+
+    def close(self):
+        try:
+            self._f.close()
+            self._sock.close()
+        except OSError:
+            pass
+        if self._srv is not None:
+            with self.cond:
+                self.closed = True
+                self.cond.notify_all()
+            self._srv.shutdown()
+            self._srv.server_close()
+            self._srv = None
+
+    __del__ = close
+
+
+class _FileStore:
+    """Rank 0 publishes the id in a file named after the ranks' common parent process
+    (torchrun's agent on this node) and the launch's port, the others wait for it; the
+    file is removed when rank 0's communicator closes (every rank has read it by then:
+    ncclCommInitRank is collective)."""
+
+    def __init__(self, tag: str, rank: int, timeout: float):
+        self.dir, self.tag, self.rank, self.timeout, self.paths = tempfile.gettempdir(), tag, rank, timeout, []
+
+    def _path(self, key: str) -> str:
+        safe = "".join(c if c.isalnum() else "_" for c in key)
+        return os.path.join(self.dir, f"wost_uid.{self.tag}.{safe}")
+
+    def set(self, key: str, value: bytes):
+        path = self._path(key)
+        tmp = f"{path}.tmp.{os.getpid()}"
+        with open(tmp, "wb") as f:
+            f.write(bytes(value))
+        os.replace(tmp, path)
+        self.paths.append(path)
+
+    def get(self, key: str) -> bytes:
+        path = self._path(key)
+        t0 = time.time()
+        while True:
+            try:
+                with open(path, "rb") as f:
+                    return f.read()
+            except OSError:
+                if time.time() - t0 > self.timeout:
+                    raise TimeoutError(f"no communicator id in {path} after {self.timeout} s") from None
+                time.sleep(0.02)
+
+    def close(self):
+        for p in self.paths:
+            try:
+                os.remove(p)
+            except OSError:
+                pass
+        self.paths = []
+
+
+def launch_store(timeout: float = 300.0):
+    """The id exchange channel of this launch (module docstring): a SocketStore hosted by
+    rank 0 on MASTER_PORT, a per-node file under torchrun's agent, or -- multi-node
+    torchrun only -- torch's TCPStore client of the agent's store."""
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    if not agent:
+        return SocketStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
+                           is_master=(rank == 0), timeout=timeout)
+    if int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == world:   # one node: the ranks share the agent as parent
+        tag = f"{os.getppid()}.{os.environ.get('MASTER_PORT', '0')}.{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
+        return _FileStore(tag, rank, timeout)
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    return dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
+                         is_master=False, timeout=timedelta(seconds=timeout))
 
 
 def shard_walk_range(walks_per_point: int, n_ranks: int, rank: int) -> tuple[int, int]:
@@ -31,20 +208,13 @@ def shard_walk_range(walks_per_point: int, n_ranks: int, rank: int) -> tuple[int
 
 
 def exchange_over_store(make_id, key: str = "wost_comm_uid", timeout: float = 300.0, store=None):
-    """Rank 0 publishes make_id() under `key` in the TCP store at MASTER_ADDR:MASTER_PORT,
-    every rank reads it back: (bytes, store). Under torchrun's elastic agent the store
-    already listens on MASTER_PORT (TORCHELASTIC_USE_AGENT_STORE) and every rank joins
-    it as a client; otherwise rank 0 hosts it. The key is scoped by the run id and
-    restart count, so a restarted job never reads a stale id."""
-    from datetime import timedelta
-
-    import torch.distributed as dist
-
-    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
-    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
-    if store is None:   # (a second id -- a second communicator -- reuses the first one's store)
-        store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
-                              is_master=(rank == 0 and not agent), timeout=timedelta(seconds=timeout))
+    """Rank 0 publishes make_id() under `key` in the launch's store (launch_store: no
+    PyTorch unless a multi-node torchrun job), every rank reads it back: (bytes, store).
+    The key is scoped by the run id and restart count, so a restarted job never reads a
+    stale id. A further id (a second communicator) passes the first one's store."""
+    rank = int(os.environ.get("RANK", "0"))
+    if store is None:
+        store = launch_store(timeout)
     k = f"{key}/{os.environ.get('TORCHELASTIC_RUN_ID', '')}/{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
     if rank == 0:
         store.set(k, make_id())
@@ -94,9 +264,11 @@ class Communicator:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         if world == 1 and "MASTER_PORT" not in os.environ:   # a lone process: no store needed
             return cls(unique_id(), 1, 0, device)
+        own = store is None
         uid, store = exchange_over_store(unique_id, key, timeout, store)
         c = cls(uid, world, rank, device)
         c._store = store   # keep the store (and, on rank 0, its server) alive with the communicator
+        c._owns_store = own
         return c
 
     @classmethod
@@ -126,6 +298,10 @@ class Communicator:
         if getattr(self, "_c", None) is not None and self._c.value:
             _lib.lib.wost_comm_destroy(self._c)
             self._c = None
+        st = getattr(self, "_store", None)
+        if st is not None and getattr(self, "_owns_store", False) and hasattr(st, "close"):
+            st.close()
+        self._store = None
 
     __del__ = close
 

@@ -412,6 +412,85 @@ def wenner_batches(n_electrodes: int, a: int = 1, max_sources: int = 16):
             yield j0, j1, t0, t1
 
 
+def group_seed(seed: int, g: int) -> int:
+    """Seed of Wenner group g: groups' walk ids stay independent."""
+    return (int(seed) * 0x9E3779B1 + g) & (2**64 - 1)
+
+
+def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent=True):
+    """The model and background fields of a multi-source survey across the ranks of one
+    communicator. Worker threads (one per field, or one for both without ``concurrent``)
+    solve this rank's walk range of every group (WostSolver_2D.solve_range with the
+    group's sources installed) and hand the block rows over; THIS thread then runs
+    libwost's protocol (distributed.run_protocol: agreement all-reduce, all-gather,
+    ordered merge) for group 0 model, group 0 background, group 1 model, ... -- the same
+    collective sequence on every rank, whatever the threads' timing. A local failure
+    travels through the protocol's agreement (every rank raises; no rank waits)."""
+    import queue
+    import threading
+
+    from . import _lib
+    from .comm import shard_walk_range
+    from .distributed import run_protocol
+    from .solvers.WoStSolver import SolveStats, _stats_of_multi
+
+    R, rank = int(comm.n_ranks), int(comm.rank)
+    w0, w1 = shard_walk_range(int(n_walks), R, rank)
+    G = len(batches)
+    slots = [[queue.Queue(maxsize=1) for _ in range(G)] for _ in range(2)]
+    stop = threading.Event()
+
+    def local(fields):
+        for g, (j0, j1, t0, t1) in enumerate(batches):
+            for f in fields:
+                if stop.is_set():
+                    slots[f][g].put((None, RuntimeError("survey stopped"), None))
+                    continue
+                s = solvers[f]
+                try:
+                    if len(srcs[t0:t1]) > _lib.WOST_MAX_SOURCES:
+                        raise ValueError(f"group {g} needs {t1 - t0} sources (> {_lib.WOST_MAX_SOURCES})")
+                    blocks, tm = None, {"total_steps": 0, "walk_kernel_ms": 0.0, "total_ms": 0.0}
+                    if w1 > w0:
+                        with s.sources_installed(s.source_fields(srcs[t0:t1])):
+                            blocks = s.solve_range(sc.points[j0:j1], int(n_walks), w0, w1, sc.max_steps, sc.eps,
+                                                   group_seed(seed, g))
+                            tm = s.last_timing
+                    slots[f][g].put((blocks, None, tm))
+                except Exception as e:   # noqa: BLE001 -- reported through the protocol
+                    slots[f][g].put((None, e, None))
+
+    groups = [(0,), (1,)] if concurrent else [(0, 1)]
+    threads = [threading.Thread(target=local, args=(fs,), daemon=True) for fs in groups]
+    for t in threads:
+        t.start()
+    try:
+        for g, (j0, j1, t0, t1) in enumerate(batches):
+            S = t1 - t0
+            for f in (0, 1):
+                blocks, err, tm = slots[f][g].get()
+
+                def solve_range(a, b, blocks=blocks, err=err):
+                    if err is not None:
+                        raise err
+                    if (a, b) != (w0, w1):
+                        raise ValueError(f"protocol asked for walks [{a}, {b}), this rank solved [{w0}, {w1})")
+                    return blocks
+
+                sums, _, all_steps = run_protocol(R, rank, j1 - j0, int(n_walks), 2 * S + 1, solve_range,
+                                                  comm.allreduce, comm.allgather)
+                stats = _stats_of_multi(sums, int(n_walks))
+                st = SolveStats(mean=np.stack([x.mean for x in stats]), stderr=np.stack([x.stderr for x in stats]),
+                                mean_steps=stats[0].mean_steps, walks=int(n_walks), total_steps=int(all_steps),
+                                kernel_ms=float(tm["walk_kernel_ms"]) if tm else 0.0,
+                                total_ms=float(tm["total_ms"]) if tm else 0.0)
+                record(f, g, st, int(tm["total_steps"]) if tm else 0)
+    finally:
+        stop.set()
+        for t in threads:   # the workers only solve locally: they always finish
+            t.join()
+
+
 def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, width: float = 0.5, seed: int = 0,
                       device: int | None = None, solvers=None, concurrent: bool = True,
                       comm=None) -> WennerSurveyResult:
@@ -427,11 +506,12 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
     walk counts. The results do not depend on it.
 
     ``comm`` (collective; every rank calls with the same arguments): a
-    dcrmontecarlo_amd.comm.Communicator -- every group is solved across its ranks by
-    walk ranges (comm.solve_sources_distributed), the results bitwise the one-GPU
-    survey's; the fields then run one after the other -- or a pair of communicators
-    (model, background) over the same ranks, which lets the two fields run
-    concurrently again, each in its own thread on its own communicator."""
+    dcrmontecarlo_amd.comm.Communicator (or any object with its ``n_ranks``, ``rank``,
+    ``allreduce`` and ``allgather``). Every group is solved across the ranks by walk
+    ranges, the results bitwise the one-GPU survey's (_run_fields_distributed): the two
+    fields' local walk-range solves run concurrently in two threads, while ONE thread
+    issues every collective, in a fixed order -- group by group, model before
+    background -- so that no two ranks can interleave them differently."""
     E = len(sc.points)
     quad = wenner_quadripoles(E, a)
     Q = len(quad)
@@ -439,36 +519,32 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
     if solvers is None:
         sm = sc.solver(device=device)
         solvers = (sm, homogeneous_solver(sc, alpha_bg, sm, device=device))
-    comms = (None, None)
-    if comm is not None:
-        comms = tuple(comm) if isinstance(comm, (tuple, list)) else (comm, comm)
-        concurrent = concurrent and comms[0] is not comms[1]
+    if isinstance(comm, (tuple, list)):
+        raise ValueError("run_wenner_survey takes one communicator: the fields' collectives are issued in a fixed "
+                         "order on it (a pair of communicators driven from two threads can deadlock)")
     mean = [np.full((Q, E), np.nan), np.full((Q, E), np.nan)]
     se = [np.full((Q, E), np.nan), np.full((Q, E), np.nan)]
     batches = list(wenner_batches(E, a))
     acc = [[0, 0.0, 0], [0, 0.0, 0]]   # per field: walk-steps (all ranks), walk-kernel ms, walk-steps (this rank)
 
+    def record(f, g, st, local):
+        j0, j1, t0, t1 = batches[g]
+        mean[f][t0:t1, j0:j1] = st.mean
+        se[f][t0:t1, j0:j1] = st.stderr
+        acc[f][0] += st.total_steps
+        acc[f][1] += st.kernel_ms
+        acc[f][2] += local
+
     def field(f):
         s = solvers[f]
         for g, (j0, j1, t0, t1) in enumerate(batches):
-            gseed = (int(seed) * 0x9E3779B1 + g) & (2**64 - 1)
-            if comms[f] is None:
-                _, st = s.solve_sources(sc.points[j0:j1], srcs[t0:t1], nWalks=n_walks, maxSteps=sc.max_steps,
-                                        eps=sc.eps, seed=gseed, return_stats=True)
-                local = st.total_steps
-            else:
-                from .comm import solve_sources_distributed
+            _, st = s.solve_sources(sc.points[j0:j1], srcs[t0:t1], nWalks=n_walks, maxSteps=sc.max_steps,
+                                    eps=sc.eps, seed=group_seed(seed, g), return_stats=True)
+            record(f, g, st, st.total_steps)
 
-                _, st, tm = solve_sources_distributed(s, comms[f], sc.points[j0:j1], srcs[t0:t1], n_walks,
-                                                      sc.max_steps, sc.eps, seed=gseed)
-                local = tm["total_steps"]
-            mean[f][t0:t1, j0:j1] = st.mean
-            se[f][t0:t1, j0:j1] = st.stderr
-            acc[f][0] += st.total_steps
-            acc[f][1] += st.kernel_ms
-            acc[f][2] += local
-
-    if concurrent:
+    if comm is not None:
+        _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent)
+    elif concurrent:
         from concurrent.futures import ThreadPoolExecutor
 
         with ThreadPoolExecutor(max_workers=2) as ex:

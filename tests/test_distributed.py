@@ -167,42 +167,66 @@ def test_walk_range_shards_match_the_library():
 
 
 # ---------------------------------------------------------------- communicator bootstrap
-def _store_worker(rank, world, port, agent, out_q):
+class _NoTorch:
+    """A meta-path finder that refuses every import of torch (the product bootstrap must
+    not need it)."""
+
+    def find_spec(self, name, path=None, target=None):
+        if name == "torch" or name.startswith("torch."):
+            raise ImportError(f"torch is blocked in this test ({name})")
+        return None
+
+
+def _store_worker(rank, world, port, mode, out_q):
     import sys
 
+    if mode in ("socket", "agent_file"):
+        for m in [m for m in sys.modules if m == "torch" or m.startswith("torch.")]:
+            del sys.modules[m]
+        sys.meta_path.insert(0, _NoTorch())
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from dcrmontecarlo_amd import comm
 
+    agent = mode != "socket"
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                      TORCHELASTIC_RUN_ID="t1", TORCHELASTIC_USE_AGENT_STORE="True" if agent else "False")
+                      TORCHELASTIC_RUN_ID="t1", TORCHELASTIC_USE_AGENT_STORE="True" if agent else "False",
+                      LOCAL_WORLD_SIZE=str(world if mode == "agent_file" else 1))
     uid, store = comm.exchange_over_store(lambda: bytes(range(128)) if rank == 0 else b"wrong", timeout=60)
-    out_q.put((rank, uid))
+    out_q.put((rank, uid, "torch" in sys.modules, type(store).__name__))
     store.set(f"done{rank}", b"1")
-    if rank == 0 and not agent:   # the host of the store outlives every reader
+    if rank == 0:   # the host of the store (or the writer of the file) outlives every reader
         for r in range(world):
             store.get(f"done{r}")
+        if hasattr(store, "close"):
+            store.close()
 
 
-@pytest.mark.parametrize("agent", [False, True])
-def test_communicator_id_travels_through_the_launch_store(agent):
+@pytest.mark.parametrize("mode", ["socket", "agent_file", "agent_tcp"])
+def test_communicator_id_travels_through_the_launch_store(mode):
     """Communicator.from_env's id exchange (the part that needs no GPU): rank 0's 128 bytes
-    reach every rank, with rank 0 hosting the store or torchrun's agent hosting it."""
+    reach every rank -- rank 0 hosting the standard-library socket store (bench.py's own
+    launcher; torch import blocked), the ranks of one torchrun node meeting in a file
+    (torch import blocked), or a multi-node torchrun agent's TCPStore."""
     from datetime import timedelta
 
     world = 3
     port = _free_port()
     host = dist.TCPStore("127.0.0.1", port, None, is_master=True, timeout=timedelta(seconds=60),
-                         wait_for_workers=False) if agent else None
+                         wait_for_workers=False) if mode == "agent_tcp" else None
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_store_worker, args=(r, world, port, agent, q)) for r in range(world)]
+    procs = [ctx.Process(target=_store_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert all(res[r] == bytes(range(128)) for r in range(world))
+    assert all(res[r][0] == bytes(range(128)) for r in range(world))
+    want = {"socket": "SocketStore", "agent_file": "_FileStore", "agent_tcp": "TCPStore"}[mode]
+    assert all(res[r][2] == want for r in range(world)), res
+    if mode != "agent_tcp":
+        assert not any(res[r][1] for r in range(world)), "torch was imported"
     del host
 
 
