@@ -54,15 +54,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["dcr_dipole", "wenner_topography"], default="dcr_dipole")
+    ap.add_argument("--workload", choices=["dcr_dipole", "wenner_topography", "variable_coefficients"],
+                    default="dcr_dipole")
     ap.add_argument("--walks", type=int, default=None,
-                    help="walks per electrode per GPU (dcr_dipole 1M, wenner_topography 100k)")
+                    help="walks per electrode per GPU (dcr_dipole 1M, wenner_topography 100k, "
+                         "variable_coefficients 100k per point)")
     ap.add_argument("--fields", choices=["literal", "physical"], default="literal",
                     help="wenner_topography: the notebook's conductivity with its air term (literal, SURVEY 8d "
                          "C5; the timed survey) or without it (physical); the rho_a report always comes from "
                          "a physical survey")
     ap.add_argument("--no-bruteforce", action="store_true", help="wenner_topography: skip the scan-kernel leg")
-    ap.add_argument("--electrodes", type=int, default=None, help="dcr_dipole 48, wenner_topography 256")
+    ap.add_argument("--electrodes", type=int, default=None,
+                    help="dcr_dipole 48, wenner_topography 256, variable_coefficients 256 (query points)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: N x --walks walks per electrode on N GPUs (default); strong: --walks on N GPUs")
@@ -129,7 +132,7 @@ def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
             break
         w = int(min(1_000_000, w * max(2.0, 0.8 * budget_s / max(dt, 1e-3))))
     base = {"value": float(s.sum()) / dt, "unit": "walk-steps/s", "cores": threads, "kind": "port",
-            "sample": f"dcr_dipole {len(pts)} electrodes x {w} walks ({int(s.sum())} walk-steps, {dt:.1f} s), "
+            "sample": f"{sc.name} {len(pts)} points x {w} walks ({int(s.sum())} walk-steps, {dt:.1f} s), "
                       f"oracle/wost_oracle.c with {threads} OpenMP threads (every usable host core)",
             "host": info}
     # the same oracle on one core, on a smaller sample (all cores and one core)
@@ -139,6 +142,8 @@ def cpu_leg(sc, sc_h, sigma_bar, sigma_bar_h, budget_s: float):
     dt1 = time.perf_counter() - t0
     base["single_core"] = {"value": float(s1.sum()) / dt1, "cores": 1,
                            "sample": f"{len(pts)} electrodes x {w1} walks ({int(s1.sum())} walk-steps, {dt1:.1f} s)"}
+    if sc_h is None:   # no apparent-resistivity leg (variable_coefficients)
+        return base, w, _point_stats(v, w), None
     vh, _ = O.Problem.from_scenario(sc_h, sigma_bar=sigma_bar_h).solve_walks(pts, w, sc.max_steps, sc.eps, CPU_SEED,
                                                                              threads=threads)
     return base, w, _point_stats(v, w), _point_stats(vh, w)
@@ -236,10 +241,10 @@ def rho_report(survey, alpha_bg, gpu_full, gpu_same, cpu_same, w_cpu, paired=Non
     return out
 
 
-def measured_traffic():
+def measured_traffic(workload: str = "dcr_dipole"):
     """HBM bytes per walk-kernel launch from the committed rocprofv3 PMC passes of this
     workload (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE), if present."""
-    path = os.path.join(REPO, "profiles", "traffic_dcr_dipole.json")
+    path = os.path.join(REPO, "profiles", f"traffic_{workload}.json")
     try:
         with open(path) as f:
             return json.load(f)["hbm_bytes_per_launch"]
@@ -247,12 +252,12 @@ def measured_traffic():
         return None
 
 
-def issue_line(perfmodel, kernel_steps_per_s: float):
+def issue_line(perfmodel, kernel_steps_per_s: float, workload: str = "dcr_dipole"):
     """The VALU issue-rate roofline of the walk kernel: instructions per wave-step from
-    the committed rocprofv3 PMC passes of this workload (profiles/issue_dcr_dipole.json),
+    the committed rocprofv3 PMC passes of this workload (profiles/issue_<workload>.json),
     at this run's kernel walk-steps/s."""
     try:
-        with open(os.path.join(REPO, "profiles", "issue_dcr_dipole.json")) as f:
+        with open(os.path.join(REPO, "profiles", f"issue_{workload}.json")) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
         return None
@@ -360,8 +365,9 @@ def main():
         return
     if args.workload == "wenner_topography":
         return wenner_main(args, world, rank, local)
-    args.walks = args.walks or 1_000_000
-    args.electrodes = args.electrodes or 48
+    c3 = args.workload == "variable_coefficients"
+    args.walks = args.walks or (100_000 if c3 else 1_000_000)
+    args.electrodes = args.electrodes or (256 if c3 else 48)
 
     from dcrmontecarlo_amd import comm as C
     from dcrmontecarlo_amd import perfmodel
@@ -369,7 +375,12 @@ def main():
     from dcrmontecarlo_amd import survey
     from dcrmontecarlo_amd.solvers.WoStSolver import stats_from_sums
 
-    sc = S.dcr_dipole(n_electrodes=args.electrodes, n_walks=args.walks)
+    if c3:   # BASELINE configs[2] / SURVEY 8d C3: 256 points x 100k walks
+        sc = S.variable_coefficients(n_points=args.electrodes, n_walks=args.walks)
+        if len(sc.points) != args.electrodes:
+            sys.exit(f"bench.py: variable_coefficients has {len(sc.points)} query points, not {args.electrodes}")
+    else:
+        sc = S.dcr_dipole(n_electrodes=args.electrodes, n_walks=args.walks)
     solver = sc.solver(device=local)
     # libwost's own RCCL communicator (wost_comm_*): the 128-byte id travels through the
     # launcher's TCP store; barriers, the block-sum all-gather and the max over ranks
@@ -422,9 +433,9 @@ def main():
 
     # apparent resistivity (second half of the metric), outside the timed region: the
     # homogeneous-background survey on the same walk streams as the last timed step
-    sc_h = survey.homogeneous(sc, ALPHA_BG)
+    sc_h = None if c3 else survey.homogeneous(sc, ALPHA_BG)
     solver_h = sums_h = None
-    if not args.no_rho:
+    if not args.no_rho and not c3:
         solver_h = survey.homogeneous_solver(sc, ALPHA_BG, solver, device=local)
         one_step(args.steps - 1, solver_h)
         sums_h = solver_h.last_point_sums
@@ -451,8 +462,12 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (reference DCR scenario fields/geometry, Philox4x32-10 walks)",
-            "config": {"workload": "dcr_dipole (testGeophysicalScenario fields, eps=0.9, maxSteps=500)",
+            "data": ("synthetic (testWostVariableCoefficients fields/geometry, Philox4x32-10 walks)" if c3 else
+                     "synthetic (reference DCR scenario fields/geometry, Philox4x32-10 walks)"),
+            "config": {"workload": ("variable_coefficients: BASELINE configs[2] / SURVEY 8d C3 (testWostVariable"
+                                    "Coefficients fields, mixed boundary with the 32-segment Neumann circle, delta "
+                                    "tracking, eps=1e-4, maxSteps=1000; points = query points)" if c3 else
+                                    "dcr_dipole (testGeophysicalScenario fields, eps=0.9, maxSteps=500)"),
                        "electrodes": len(sc.points), "walks_per_electrode": Wt,
                        "walks_per_electrode_per_gpu": w1 - w0,
                        "walk_steps_per_solve": total_steps // max(args.steps, 1),
@@ -463,24 +478,29 @@ def main():
                          "unit": "TFLOP/s", "frac": ach_tflops / perfmodel.FP32_PEAK_TFLOPS,
                          # HBM bytes per walk-kernel launch from the committed PMC passes
                          # (profiles/traffic_dcr_dipole.json) vs the algorithmic 8 B per walk
-                         "traffic": measured_traffic(), "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "model_flops_per_step": fps, "flop_model": "SURVEY.md 8(d) v1 per-config total (C4 ~350)",
+                         "traffic": measured_traffic(args.workload),
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "model_flops_per_step": fps,
+                         "flop_model": "SURVEY.md 8(d) v1 per-config total (C3 ~1,150, C4 ~350)",
                          # the same model without the ~120 FLOP i0e series the kernel replaced by
                          # an LDS table lookup: the FP32 work it executes
                          "executed_flops_per_step": fps_exec, "achieved_executed": exec_tflops,
                          "frac_executed": exec_tflops / perfmodel.FP32_PEAK_TFLOPS,
-                         "kernel": "wost_walk_jit (hiprtc field-specialised, mixed+delta)" if jit
+                         "kernel": f"wost_walk_jit (hiprtc field-specialised, mixed+delta, {args.workload})" if jit
                          else "wost_walk_kernel<true,true,true> (precompiled)",
                          "kernel_ms_per_launch": kernel_ms / max(launches, 1),
-                         "issue": issue_line(perfmodel, steps_local / (kernel_ms * 1e-3) if kernel_ms > 0 else 0.0)},
+                         "issue": issue_line(perfmodel, steps_local / (kernel_ms * 1e-3) if kernel_ms > 0 else 0.0,
+                                             args.workload)},
             "roofline_hbm": {"bound": "hbm", "achieved": ach_gbs, "peak": perfmodel.HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": ach_gbs / perfmodel.HBM_PEAK_GBS, "traffic": measured_traffic(),
+                             "frac": ach_gbs / perfmodel.HBM_PEAK_GBS, "traffic": measured_traffic(args.workload),
                              "algorithmic_bytes_per_launch": bytes_per_launch},
             "u_checksum": float(np.sum(mean)),
         }
         cpu_same = gpu_same = None
         w_cpu = 0
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu and world == 1 and c3:
+            out["cpu_baseline"] = cpu_leg(sc, None, solver.sigma_bar or 0.0, 0.0, args.cpu_seconds)[0]
+        elif not args.no_cpu and world == 1:
             if solver_h is None:
                 solver_h = survey.homogeneous_solver(sc, ALPHA_BG, solver, device=local)
             base, w_cpu, cm, ch = cpu_leg(sc, sc_h, solver.sigma_bar or 0.0, solver_h.sigma_bar or 0.0,
@@ -494,7 +514,7 @@ def main():
             gpu_same = ((gm.mean, gm.stderr), (gh.mean, gh.stderr))
         else:
             out["cpu_baseline"] = None
-        if not args.no_rho:
+        if not args.no_rho and not c3:
             st_m, st_h = stats_from_sums(last_sums, Wt), stats_from_sums(sums_h, Wt)
             gpu_full = ((st_m.mean, st_m.stderr), (st_h.mean, st_h.stderr), Wt)
             paired = paired_walks(survey, sc, solver, solver_h, RHO_REPLICA_WALKS * RHO_REPLICAS)

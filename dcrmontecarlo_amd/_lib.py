@@ -22,7 +22,7 @@ WOST_ERR_UNSUPPORTED = -4
 WOST_ERR_OOM = -5
 WOST_ERR_COMM = -6
 
-ABI_VERSION = 3   # include/wost.h WOST_ABI_VERSION
+ABI_VERSION = 4   # include/wost.h WOST_ABI_VERSION
 WOST_COMM_ID_BYTES = 128
 WOST_COMM_SUM, WOST_COMM_MAX = 0, 1
 WOST_BLOCK_WALKS = 4096
@@ -32,6 +32,7 @@ COMPAT = {"reference": 0, "fixed": 1}
 SLOT_BOUNDARY, SLOT_SOURCE = 0, 1
 GEOM_OPS = {"distance": 0, "isSilhouette": 1, "silhouetteDistance": 2, "rayIntersection": 3,
             "intersectPolylines": 4}
+WOST_GEOM_TREE = 256   # wost_geom_op flag: the query through the segment tree (ops 2 and 4)
 
 
 class WostFactor(ctypes.Structure):
@@ -78,7 +79,8 @@ DIST_ALLGATHER = ctypes.CFUNCTYPE(c_int32, c_void_p, POINTER(c_double), c_int64,
 class WostDistOps(ctypes.Structure):
     """include/wost.h wost_dist_ops: the transport of wost_distributed_run."""
     _fields_ = [("ctx", c_void_p), ("prepare", DIST_PREPARE), ("solve_range", DIST_SOLVE_RANGE),
-                ("allreduce", DIST_ALLREDUCE), ("allgather", DIST_ALLGATHER)]
+                ("allreduce", DIST_ALLREDUCE), ("allgather", DIST_ALLGATHER), ("key", POINTER(c_double)),
+                ("n_key", c_int32)]
 
 
 class WostError(RuntimeError):
@@ -133,10 +135,12 @@ def _load():
         "wost_distributed_run": (c_int32, [POINTER(WostDistOps), c_int32, c_int32, c_int64, c_int64, c_int32,
                                            POINTER(c_double), POINTER(c_int64), POINTER(c_int64),
                                            POINTER(c_uint64)]),
+        "wost_dist_solve_key": (c_int32, [c_uint64, c_float, c_int32, POINTER(c_float), c_int64, POINTER(c_double)]),
         "wost_greens_norm": (c_int32, [c_double, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_screened_sample_fixed": (c_int32, [POINTER(c_float), POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_screened_cdf_fixed": (c_int32, [c_double, POINTER(c_double), c_int64, POINTER(c_double)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
+        "wost_set_fixed_step_check": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
         "wost_kernel_source": (c_int32, [POINTER(WostProblem), ctypes.c_char_p, c_int64, POINTER(c_int64)]),
         "wost_eval_field": (c_int32, [H, c_int32, POINTER(c_float), c_int64, POINTER(c_float)]),

@@ -188,6 +188,9 @@ struct wost_handle {
     bool prog_dirty = true;
     uint64_t prog_version = 0;  // bumped whenever the program is rebuilt
 
+    // compat="fixed" delta tracking: refuse solves whose walks would all hit maxSteps
+    bool fixed_step_check = true;
+
     // field-specialised walk kernel (wost_jit.cpp)
     bool jit_enabled = true;
     hipFunction_t jit_fn = nullptr;
@@ -255,10 +258,12 @@ int upload_program(wost_handle* h) {
 // when `record`), or nullptr when it is disabled or could not be built (the
 // precompiled kernel is used then; same results).
 hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock,
-                         bool global_polylines = false) {
+                         bool global_polylines = false, int tree_stage = 0) {
     if (!h->jit_enabled) return nullptr;
-    const int bk = block == kWalkBlock ? 0 : block == kTreeStageBlock ? 1 : block == kTreeStageVertsBlock ? 2 : 3;
-    const int key = (((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 4 + bk) * 2 + (global_polylines ? 1 : 0);
+    // the cache key holds everything the source depends on: the staging level and the
+    // exact workgroup size (a multiple of 64, at most 1024)
+    const int key = ((((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 3 + tree_stage) * 17 +
+                     block / 64) * 2 + (global_polylines ? 1 : 0);
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
     h->jit_alpha_fn = nullptr;
@@ -273,7 +278,7 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
     }
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
                                          (int)(h->dverts.size() / 2), h->nverts.data(), nn, record, ns, block,
-                                         phi.empty() ? nullptr : phi.data(), global_polylines);
+                                         phi.empty() ? nullptr : phi.data(), global_polylines, tree_stage);
     std::string err;
     hipFunction_t fn = nullptr;
     hipFunction_t afn = nullptr;
@@ -760,6 +765,30 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         return fail(WOST_ERR_INVALID_ARG,
                     "delta tracking (sigma/alpha given) needs a source term: the reference raises "
                     "UnboundLocalError at solvers/WoStSolver.py:281 (quirk Q14)");
+    if (h->compat == WOST_COMPAT_FIXED && h->delta && h->fixed_step_check && n_points > 0 && max_steps > 0 &&
+        h->dverts.size() >= 4) {
+        // compat="fixed" delta tracking draws each collision from the ball's own screened
+        // law: with R sqrt(sigma_bar) >> 1 a step moves ~2/sqrt(sigma_bar) (E[l^2] = 4 /
+        // sigma_bar), so leaving a point at Dirichlet distance d takes ~d^2 sigma_bar / 4
+        // steps. When that exceeds maxSteps at the median point, every walk would end
+        // truncated at maxSteps (the DCR configurations: sigma_bar = 10, d ~ 100): refuse.
+        std::vector<double> est((size_t)n_points);
+        const auto* dv = reinterpret_cast<const float2*>(h->dverts.data());
+        const int nd = (int)(h->dverts.size() / 2);
+        for (int64_t i = 0; i < n_points; ++i) {
+            const double d = poly_distance(dv, nd, points[2 * i], points[2 * i + 1]);
+            est[(size_t)i] = d * d * h->sigma_bar / 4.0;
+        }
+        std::nth_element(est.begin(), est.begin() + n_points / 2, est.end());
+        const double med = est[(size_t)(n_points / 2)];
+        if (med > (double)max_steps)
+            return fail(WOST_ERR_INVALID_ARG,
+                        "compat=\"fixed\" delta tracking would truncate the walks: at the median query point a walk "
+                        "needs ~%.3g steps (d^2 sigma_bar / 4, sigma_bar = %g) to reach the Dirichlet boundary, "
+                        "maxSteps is %d; raise maxSteps, lower sigma_bar, or disable this check "
+                        "(wost_set_fixed_step_check / WostSolver_2D.set_fixed_step_check(False))",
+                        med, h->sigma_bar, (int)max_steps);
+    }
     const int mode = walk_mode(h);
     const bool src = h->fields[SLOT_F].present;
 
@@ -816,7 +845,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     // (the staged tree records have their own budget, kTreeLdsMaxBytes)
     const bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0,
                                                         jit_const_dirichlet(nd_)) > kGlobalPolylineLdsBytes;
-    hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly);
+    auto stage_of = [](int recs, int verts) { return recs > 0 ? (verts > 0 ? 2 : 1) : 0; };
+    hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts));
     if (!jfn && block != kWalkBlock) {   // the precompiled kernels run 256-thread workgroups, no staged tree
         block = kWalkBlock;
         tree_lds = 0;
@@ -830,14 +860,23 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     // A/B knob (occupancy studies): WOST_LDS_PAD_BYTES extra bytes of LDS per workgroup
     if (const char* e = std::getenv("WOST_LDS_PAD_BYTES")) lds += (size_t)std::max(0, std::atoi(e));
     int blocks_per_cu = 0;
-    if (jfn)
-        HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
+    // a workgroup whose LDS exceeds the CU's never fits: checked here, not left to the
+    // occupancy query
+    int lds_cap = 0;
+    HIP_TRY(hipDeviceGetAttribute(&lds_cap, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device));
+    auto occupancy = [&]() -> hipError_t {
+        blocks_per_cu = 0;
+        if (lds > (size_t)lds_cap) return hipSuccess;
+        return hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds);
+    };
+    if (jfn) HIP_TRY(occupancy());
     while (jfn && tree_lds > 0 && blocks_per_cu * (block / 64) < 16) {
-        // what the tree stages leaves fewer than 16 waves per CU: stage less (the vertices,
-        // then the records), down to reading both through L1/L2 from 256-thread workgroups
+        // what the tree stages leaves fewer than 16 waves per CU (or does not fit at all):
+        // stage less (the vertices, then the records), down to reading both through L1/L2
+        // from 256-thread workgroups
         tree_level = tree_verts > 0 ? 1 : 0;
         tree_lds = tree_lds_records(h, mode, tree_level, &block, &tree_verts);
-        if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly))) {
+        if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts)))) {
             // the precompiled kernels then (256-thread workgroups, nothing of the tree staged)
             block = kWalkBlock;
             tree_lds = tree_verts = 0;
@@ -848,7 +887,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         }
         lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jit_const_dirichlet(nd_),
                              jit_const_neumann(mode, nn_), gpoly, block, tree_verts);
-        HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, jfn, block, lds));
+        HIP_TRY(occupancy());
     }
     if (!jfn)
         HIP_TRY(walk_occupancy(mode, (int)(h->dverts.size() / 2), (int)(h->nverts.size() / 2), (int)n_points,
@@ -1174,6 +1213,12 @@ int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_seg
     return WOST_OK;
 }
 
+int wost_set_fixed_step_check(wost_handle* h, int32_t enable) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    h->fixed_step_check = enable != 0;
+    return WOST_OK;
+}
+
 int wost_set_jit(wost_handle* h, int32_t enable) {
     if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
     h->jit_enabled = enable != 0;
@@ -1206,8 +1251,13 @@ int wost_eval_field(wost_handle* h, int32_t which, const float* points, int64_t 
 int wost_geometry_query(int32_t device, int32_t op, const wost_polyline* poly, const float* points,
                         const float* dirs, const float* radii, int64_t n, float* out_f, uint8_t* out_mask) {
     if (!poly || !poly->xy || poly->n_vertices < 1) return fail(WOST_ERR_INVALID_ARG, "bad polyline");
+    const bool tree = (op & WOST_GEOM_TREE) != 0;
+    op &= ~WOST_GEOM_TREE;
     if (op < WOST_GEOM_DISTANCE || op > WOST_GEOM_INTERSECT_POLYLINES) return fail(WOST_ERR_INVALID_ARG, "unknown op %d", op);
+    if (tree && op != WOST_GEOM_SILHOUETTE_DISTANCE && op != WOST_GEOM_INTERSECT_POLYLINES)
+        return fail(WOST_ERR_INVALID_ARG, "the segment tree answers silhouetteDistance and intersectPolylines only");
     const int nv = poly->n_vertices;
+    if (tree && nv < 3) return fail(WOST_ERR_INVALID_ARG, "the segment tree needs >= 2 segments");
     if ((op == WOST_GEOM_DISTANCE || op == WOST_GEOM_RAY_INTERSECTION || op == WOST_GEOM_INTERSECT_POLYLINES) && nv < 2)
         return fail(WOST_ERR_INVALID_ARG, "op %d needs a polyline with >= 2 vertices", op);
     if (n < 0 || (n > 0 && !points)) return fail(WOST_ERR_INVALID_ARG, "bad points");
@@ -1220,7 +1270,20 @@ int wost_geometry_query(int32_t device, int32_t op, const wost_polyline* poly, c
     const int64_t nm_out = op == WOST_GEOM_IS_SILHOUETTE ? n * std::max(0, nv - 2) : 0;
     if ((nf_out > 0 && !out_f) || (nm_out > 0 && !out_mask)) return fail(WOST_ERR_INVALID_ARG, "output buffer missing");
     if (n == 0) return WOST_OK;
+    SegmentTreeHost th;
+    if (tree && !build_segment_tree(poly->xy, nv, WOST_TREE_LEAF_DEFAULT, &th) &&
+        !build_segment_tree(poly->xy, nv, 32, &th))
+        return fail(WOST_ERR_INVALID_ARG, "no segment tree for this polyline (degenerate or too long)");
     HIP_TRY(hipSetDevice(device));
+    float4* drec = nullptr;
+    if (tree) {
+        HIP_TRY(hipMalloc(&drec, sizeof(float) * std::max<size_t>(th.rec.size(), 4)));
+        const hipError_t e0 = hipMemcpy(drec, th.rec.data(), sizeof(float) * th.rec.size(), hipMemcpyHostToDevice);
+        if (e0 != hipSuccess) {
+            (void)hipFree(drec);
+            return fail(WOST_ERR_HIP, "wost_geometry_query: %s", hipGetErrorString(e0));
+        }
+    }
     float2 *dv = nullptr, *dp = nullptr, *dd = nullptr;
     float *dr = nullptr, *df = nullptr;
     uint8_t* dm = nullptr;
@@ -1234,11 +1297,14 @@ int wost_geometry_query(int32_t device, int32_t op, const wost_polyline* poly, c
     if (e == hipSuccess) e = hipMemcpy(dp, points, sizeof(float2) * n, hipMemcpyHostToDevice);
     if (e == hipSuccess && dd) e = hipMemcpy(dd, dirs, sizeof(float2) * n, hipMemcpyHostToDevice);
     if (e == hipSuccess && dr) e = hipMemcpy(dr, radii, sizeof(float) * n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = launch_geometry_query(op, dv, nv, dp, dd, dr, n, df, dm, nullptr);
+    if (e == hipSuccess)
+        e = tree ? launch_geometry_tree_query(op, dv, nv, drec, th.first_leaf, th.depth, th.leaf, th.tol, th.kmax, dp,
+                                              dd, dr, n, df, nullptr)
+                 : launch_geometry_query(op, dv, nv, dp, dd, dr, n, df, dm, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess && df) e = hipMemcpy(out_f, df, sizeof(float) * nf_out, hipMemcpyDeviceToHost);
     if (e == hipSuccess && dm) e = hipMemcpy(out_mask, dm, nm_out, hipMemcpyDeviceToHost);
-    void* all[] = {dv, dp, dd, dr, df, dm};
+    void* all[] = {dv, dp, dd, dr, df, dm, drec};
     for (void* p : all)
         if (p) (void)hipFree(p);
     if (e != hipSuccess) return fail(WOST_ERR_HIP, "wost_geometry_query: %s", hipGetErrorString(e));

@@ -214,6 +214,21 @@ int wost_shard_merge(const double* gathered, int64_t n_points, int64_t walks_per
     return WOST_OK;
 }
 
+int wost_dist_solve_key(uint64_t seed, float eps, int32_t max_steps, const float* points, int64_t n_points,
+                        double* key) {
+    if (!key || n_points < 0 || (n_points > 0 && !points)) return cfail(WOST_ERR_INVALID_ARG, "bad arguments");
+    uint64_t hsh = 1469598103934665603ull;   // FNV-1a 64 over the points' bytes
+    const auto* b = reinterpret_cast<const unsigned char*>(points);
+    for (int64_t i = 0; i < 8 * n_points; ++i) hsh = (hsh ^ b[i]) * 1099511628211ull;
+    key[0] = (double)(uint32_t)seed;
+    key[1] = (double)(uint32_t)(seed >> 32);
+    key[2] = (double)eps;
+    key[3] = (double)max_steps;
+    key[4] = (double)(uint32_t)hsh;
+    key[5] = (double)(uint32_t)(hsh >> 32);
+    return WOST_OK;
+}
+
 int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank, int64_t n_points,
                          int64_t walks_per_point, int32_t row, double* point_stats, int64_t* walk_begin,
                          int64_t* walk_end, uint64_t* total_steps) {
@@ -263,16 +278,35 @@ int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank
         }
         if (local == WOST_OK) (void)wost_shard_pack(bs.data(), n_points, walks_per_point, n_ranks, rank, row, mine.data());
     }
-    // agreement: max of (failed, n_points, -n_points, row, -row, W, -W)
-    double agree[7] = {local != WOST_OK ? 1.0 : 0.0, (double)n_points, -(double)n_points, (double)row, -(double)row,
-                       (double)walks_per_point, -(double)walks_per_point};
-    int rc = ops->allreduce(ops->ctx, agree, 7, WOST_COMM_MAX);
+    // agreement: max of (failed, n_points, -n_points, row, -row, W, -W, key[k], -key[k] ...);
+    // the key's length is part of what must agree (a rank with another n_key fails it)
+    const int nk = (ops->key && ops->n_key > 0) ? std::min<int>(ops->n_key, WOST_DIST_MAX_KEY) : 0;
+    if (ops->n_key < 0 || ops->n_key > WOST_DIST_MAX_KEY || (ops->n_key > 0 && !ops->key)) {
+        local = WOST_ERR_INVALID_ARG;
+        local_msg = "bad agreement key";
+    }
+    double agree[9 + 2 * WOST_DIST_MAX_KEY] = {local != WOST_OK ? 1.0 : 0.0, (double)n_points, -(double)n_points,
+                                               (double)row, -(double)row, (double)walks_per_point,
+                                               -(double)walks_per_point, (double)nk, -(double)nk};
+    for (int k = 0; k < nk; ++k) {
+        // NaN never agrees: map it to a value no finite key takes
+        const double v = ops->key[k] == ops->key[k] ? ops->key[k] : 1e308;
+        agree[9 + 2 * k] = v;
+        agree[10 + 2 * k] = -v;
+    }
+    const int na = 9 + 2 * WOST_DIST_MAX_KEY;   // fixed length: every rank reduces the same count
+    int rc = ops->allreduce(ops->ctx, agree, na, WOST_COMM_MAX);
     if (rc != WOST_OK) return cfail(rc, "agreement all-reduce: %s", g_comm_err.c_str());
     if (local != WOST_OK) return cfail(local, "rank %d: %s", rank, local_msg.c_str());
     if (agree[0] > 0.0) return cfail(WOST_ERR_COMM, "rank %d: another rank failed; no result", rank);
     if (agree[1] != -agree[2] || agree[3] != -agree[4] || agree[5] != -agree[6])
         return cfail(WOST_ERR_INVALID_ARG, "ranks disagree on the solve (n_points %g..%g, row %g..%g, walks %g..%g)",
                      -agree[2], agree[1], -agree[4], agree[3], -agree[6], agree[5]);
+    for (int k = 0; k < 1 + WOST_DIST_MAX_KEY; ++k)
+        if (agree[7 + 2 * k] != -agree[8 + 2 * k])
+            return cfail(WOST_ERR_INVALID_ARG,
+                         "ranks disagree on the solve's arguments (%s %d: %.17g..%.17g; seed, eps, maxSteps, points)",
+                         k == 0 ? "key length" : "key entry", k == 0 ? 0 : k - 1, -agree[8 + 2 * k], agree[7 + 2 * k]);
     if (per_rank > 0) {
         rc = ops->allgather(ops->ctx, mine.data(), (int64_t)per_rank, all.data());
         if (rc != WOST_OK) return cfail(rc, "block all-gather: %s", g_comm_err.c_str());
@@ -345,7 +379,9 @@ int wost_solve_distributed(wost_handle* h, wost_comm* c, const float* points, in
     else row = 2 * ns + 1;
     if (n_points > 0 && !points) row = 0;
     RcclRun run{h, c, points, n_points, walks_per_point, max_steps, eps, seed};
-    wost_dist_ops ops{&run, rccl_prepare, rccl_solve_range, rccl_allreduce, rccl_allgather};
+    double key[6] = {0, 0, 0, 0, 0, 0};
+    if (n_points >= 0 && (points || n_points == 0)) (void)wost_dist_solve_key(seed, eps, max_steps, points, n_points, key);
+    wost_dist_ops ops{&run, rccl_prepare, rccl_solve_range, rccl_allreduce, rccl_allgather, key, 6};
     int64_t w0 = 0, w1 = 0;
     uint64_t steps = 0;
     const int rc = wost_distributed_run(&ops, c->n_ranks, c->rank, n_points, walks_per_point, row, point_stats, &w0,

@@ -90,6 +90,11 @@ hipError_t launch_block_reduce(const float* val, const uint32_t* steps, const in
 hipError_t launch_geometry_query(int op, const float2* verts, int nv, const float2* pts,
                                  const float2* dirs, const float* radii, int64_t n,
                                  float* out_f, uint8_t* out_mask, hipStream_t s);
+// op 2 / 4 through the segment tree (records rec of SegmentTreeHost), one query per lane
+hipError_t launch_geometry_tree_query(int op, const float2* verts, int nv, const float4* rec, int first_leaf,
+                                      int depth, int leaf, float tol, float kmax, const float2* pts,
+                                      const float2* dirs, const float* radii, int64_t n, float* out_f,
+                                      hipStream_t s);
 
 // atan2 of the left normal of each of the nseg segments of verts -> phi[nseg].
 hipError_t launch_segment_phi(const float2* verts, int nseg, float* phi, hipStream_t s);

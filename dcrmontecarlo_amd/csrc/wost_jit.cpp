@@ -382,7 +382,7 @@ bool jit_const_neumann(int mode, int nn) {
 
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources,
-                         int block, const float* seg_phi, bool global_polylines) {
+                         int block, const float* seg_phi, bool global_polylines, int tree_stage) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -408,8 +408,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_TREE_SHARE " << std::max(0, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_DESCENT"))   // A/B: hand-outs during the descent
         o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
-    if (tree && block != kWalkBlock) o << "#define WOST_TREE_STAGED 1\n";   // every record in LDS
-    if (tree && block == kTreeStageVertsBlock) o << "#define WOST_TREE_VSTAGED 1\n";   // and the vertices
+    if (tree && tree_stage >= 1) o << "#define WOST_TREE_STAGED 1\n";    // every record in LDS
+    if (tree && tree_stage >= 2) o << "#define WOST_TREE_VSTAGED 1\n";   // and the Neumann vertices
     if (const char* e = std::getenv("WOST_JIT_TREE_QMARGIN"))   // A/B: per-query rounding scales
         o << "#define WOST_TREE_QMARGIN " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_MIN"))   // A/B: fewest subtrees worth a hand-out

@@ -36,11 +36,14 @@ bool jit_const_neumann(int mode, int nn);
 // device's per-segment normal angles of a compiled-in Neumann polyline (nn - 1
 // floats, read back from the setup kernel so the constants carry its bits);
 // global_polylines: the kernel reads polylines that are not compiled in from
-// global memory instead of staging them in LDS (wost_walk.h GL).
+// global memory instead of staging them in LDS (wost_walk.h GL). tree_stage (tree
+// modes): 0 = the segment tree through L1/L2, 1 = its records staged in LDS
+// (WOST_TREE_STAGED), 2 = its records and the Neumann vertices (WOST_TREE_VSTAGED) --
+// the caller's staging decision, independent of the workgroup size.
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record,
                          int n_sources = 1, int block = 256, const float* seg_phi = nullptr,
-                         bool global_polylines = false);
+                         bool global_polylines = false, int tree_stage = 0);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

@@ -303,6 +303,40 @@ hipError_t launch_geometry_query(int op, const float2* verts, int nv, const floa
     return hipGetLastError();
 }
 
+// The same queries answered by the Neumann segment tree of the walk kernels, one
+// query per lane (silhouette_distance_tree without a Dirichlet bound: exact;
+// intersect_polylines_tree, reference mode): wost_geometry_query(op | WOST_GEOM_TREE).
+__global__ void __launch_bounds__(256)
+wost_geometry_tree_kernel(int op, SegTree t, const float2* __restrict__ pts, const float2* __restrict__ dirs,
+                          const float* __restrict__ radii, int64_t n, float* __restrict__ out_f) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float2 p = pts[i];
+    if (op == WOST_GEOM_SILHOUETTE_DISTANCE) {
+        out_f[i] = silhouette_distance_tree(t, p.x, p.y, WOST_INF);
+    } else {
+        const float2 d = dirs[i];
+        const Hit h = intersect_polylines_tree(t, p.x, p.y, d.x, d.y, radii[i]);
+        out_f[5 * i + 0] = h.x;
+        out_f[5 * i + 1] = h.y;
+        out_f[5 * i + 2] = h.nx;
+        out_f[5 * i + 3] = h.ny;
+        out_f[5 * i + 4] = h.hit ? 1.f : 0.f;
+    }
+}
+
+hipError_t launch_geometry_tree_query(int op, const float2* verts, int nv, const float4* rec, int first_leaf,
+                                      int depth, int leaf, float tol, float kmax, const float2* pts,
+                                      const float2* dirs, const float* radii, int64_t n, float* out_f,
+                                      hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (op != WOST_GEOM_SILHOUETTE_DISTANCE && op != WOST_GEOM_INTERSECT_POLYLINES) return hipErrorInvalidValue;
+    SegTree t{rec, verts, nv, first_leaf, depth, leaf, tol, kmax};
+    const int64_t grid = (n + 255) / 256;
+    wost_geometry_tree_kernel<<<(unsigned)grid, 256, 0, s>>>(op, t, pts, dirs, radii, n, out_f);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Field evaluation at points: value + gradient + Laplacian, or sigma'.
 // ---------------------------------------------------------------------------

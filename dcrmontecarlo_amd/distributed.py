@@ -122,11 +122,12 @@ class _Transport:
     callback becomes an error status for the protocol (and is re-raised by
     run_protocol on the rank where it happened)."""
 
-    def __init__(self, n_points, row, solve_range, allreduce, allgather, prepare=None):
+    def __init__(self, n_points, row, solve_range, allreduce, allgather, prepare=None, n_ranks=None, key=None):
         from . import _lib
 
         self.error = None
         self.n_points, self.row = int(n_points), int(row)
+        self.n_ranks = None if n_ranks is None else int(n_ranks)
 
         def guard(fn):
             def wrapped(*a):
@@ -154,6 +155,10 @@ class _Transport:
         def _allgather(ctx, send, count, recv):
             a = np.ctypeslib.as_array(send, shape=(int(count),)).copy()
             out = np.ascontiguousarray(allgather(a), np.float64).ravel()
+            # recv holds n_ranks * count doubles: a transport whose group is not the
+            # protocol's n_ranks must not write past it
+            if self.n_ranks is not None and out.size != self.n_ranks * int(count):
+                raise ValueError(f"allgather returned {out.size} values, expected {self.n_ranks} ranks x {int(count)}")
             r = np.ctypeslib.as_array(recv, shape=(out.size,))
             r[:] = out
             return 0
@@ -165,21 +170,37 @@ class _Transport:
 
         self._cb = (_lib.DIST_PREPARE(guard(_prepare)), _lib.DIST_SOLVE_RANGE(guard(_solve)),
                     _lib.DIST_ALLREDUCE(guard(_allreduce)), _lib.DIST_ALLGATHER(guard(_allgather)))
-        self.ops = _lib.WostDistOps(None, *self._cb)
+        self._key = None if key is None else np.ascontiguousarray(key, np.float64).ravel()
+        self.ops = _lib.WostDistOps(None, *self._cb, _lib.dptr(self._key) if self._key is not None else None,
+                                    0 if self._key is None else int(self._key.size))
+
+
+def solve_key(seed: int, eps: float, max_steps: int, points) -> np.ndarray:
+    """The agreement key of a solve (wost_dist_solve_key): seed halves, eps, maxSteps and
+    a checksum of the float32 points -- values every rank must pass identically."""
+    from . import _lib
+
+    p = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1, 2))
+    key = np.zeros(6, np.float64)
+    _lib.check(_lib.lib.wost_dist_solve_key(int(seed) & (2**64 - 1), float(eps), int(max_steps), _lib.fptr(p),
+                                            p.shape[0], _lib.dptr(key)), "wost_dist_solve_key")
+    return key
 
 
 def run_protocol(n_ranks: int, rank: int, n_points: int, walks_per_point: int, row: int, solve_range, allreduce,
-                 allgather, prepare=None):
+                 allgather, prepare=None, key=None):
     """libwost's distributed protocol (wost_distributed_run: agreement all-reduce,
     all-gather of the padded block rows, ordered merge) over Python callables:
     solve_range(w0, w1) -> [n_points, blocks, row] float64 of this rank's walks;
     allreduce(a, "sum"|"max") -> a reduced; allgather(a) -> [n_ranks, a.size].
+    ``key`` (optional, <= 16 values, e.g. solve_key(...)): arguments every rank must
+    hold identically; a rank that differs makes every rank raise ValueError.
     Returns (point sums [n_points, row], (walk_begin, walk_end), total walk-steps).
     Raises the local exception on the rank whose callback failed, WostError on the
     others (no rank is left waiting in a collective)."""
     from . import _lib
 
-    tr = _Transport(n_points, row, solve_range, allreduce, allgather, prepare)
+    tr = _Transport(n_points, row, solve_range, allreduce, allgather, prepare, n_ranks=n_ranks, key=key)
     out = np.zeros((int(n_points), int(row)), np.float64)
     w0, w1, steps = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_uint64()
     rc = _lib.lib.wost_distributed_run(ctypes.byref(tr.ops), int(n_ranks), int(rank), int(n_points),
@@ -226,6 +247,7 @@ def solve_distributed(solver, points, nWalks: int, maxSteps: int = 1000, eps: fl
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     ar, ag = torch_transport(group, device)
     sums, _, steps = run_protocol(world, rank, pts.shape[0], int(nWalks), 3,
-                                  lambda w0, w1: solver.solve_range(pts, nWalks, w0, w1, maxSteps, eps, seed), ar, ag)
+                                  lambda w0, w1: solver.solve_range(pts, nWalks, w0, w1, maxSteps, eps, seed), ar, ag,
+                                  key=solve_key(seed, eps, maxSteps, pts))
     u = (sums[:, 0] / nWalks).astype(np.float32).reshape(-1, 1)
     return u, stats_from_sums(sums, nWalks, steps)

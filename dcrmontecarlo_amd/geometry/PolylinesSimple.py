@@ -50,7 +50,7 @@ class PolyLinesSimple(PolyLines):
         self._xy = xy
 
     # ------------------------------------------------------------------
-    def _query(self, op: str, point, direction=None, r=None):
+    def _query(self, op: str, point, direction=None, r=None, tree: bool = False):
         p = _np32(point)
         single = p.ndim == 1
         p = p.reshape(-1, 2)
@@ -62,7 +62,7 @@ class PolyLinesSimple(PolyLines):
             d = np.ascontiguousarray(np.broadcast_to(_np32(direction).reshape(-1, 2), (n, 2)))
         if r is not None:
             rr = np.ascontiguousarray(np.broadcast_to(np.asarray(_np32(r)).reshape(-1), (n,)))
-        code = _lib.GEOM_OPS[op]
+        code = _lib.GEOM_OPS[op] | (_lib.WOST_GEOM_TREE if tree else 0)
         out_f = out_m = None
         if op in ("distance", "silhouetteDistance"):
             out_f = np.empty(n, np.float32)
@@ -92,9 +92,10 @@ class PolyLinesSimple(PolyLines):
         m, single = self._query("isSilhouette", point)
         return _out(m[0] if single else m, point)
 
-    def silhouetteDistance(self, point):
-        """Distance to the nearest silhouette vertex, inf if none (:83-102)."""
-        v, single = self._query("silhouetteDistance", point)
+    def silhouetteDistance(self, point, *, tree: bool = False):
+        """Distance to the nearest silhouette vertex, inf if none (:83-102). ``tree``:
+        answered by the walk kernels' segment tree (same bits as the scan)."""
+        v, single = self._query("silhouetteDistance", point, tree=tree)
         if single:
             return _scalar(v[0]) if _is_torch(point) else np.float32(v[0])
         return _out(v, point)
@@ -104,9 +105,10 @@ class PolyLinesSimple(PolyLines):
         t, single = self._query("rayIntersection", point, direction)
         return _out(t[0] if single else t, point)
 
-    def intersectPolylines(self, point, direction, r):
-        """(hit point or point + r*d, normal, found) (intersect_polylines_jit, :134-197)."""
-        o, single = self._query("intersectPolylines", point, direction, r)
+    def intersectPolylines(self, point, direction, r, *, tree: bool = False):
+        """(hit point or point + r*d, normal, found) (intersect_polylines_jit, :134-197).
+        ``tree``: answered by the walk kernels' segment tree (same bits as the scan)."""
+        o, single = self._query("intersectPolylines", point, direction, r, tree=tree)
         if single:
             return _out(o[0, 0:2].copy(), point), _out(o[0, 2:4].copy(), point), bool(o[0, 4] != 0)
         return _out(o[:, 0:2].copy(), point), _out(o[:, 2:4].copy(), point), _out(o[:, 4] != 0, point)

@@ -281,6 +281,12 @@ class WostSolver_2D:
         kernel that interprets the fields. Both give identical results."""
         _lib.check(_lib.lib.wost_set_jit(self._h, 1 if enable else 0), "wost_set_jit")
 
+    def set_fixed_step_check(self, enable: bool):
+        """compat="fixed" delta tracking refuses (ValueError) a solve whose walks would all
+        hit maxSteps (~d^2 sigma_bar / 4 steps from Dirichlet distance d at the median
+        query point, wost_set_fixed_step_check); False lets such truncated solves run."""
+        _lib.check(_lib.lib.wost_set_fixed_step_check(self._h, 1 if enable else 0), "wost_set_fixed_step_check")
+
     def set_segment_tree(self, min_segments: int = 64, leaf_segments: int = 0):
         """Route the Neumann closest-silhouette and ray queries through the segment
         tree when the Neumann polyline has >= min_segments segments (< 0: never,

@@ -431,7 +431,7 @@ def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, rec
 
     from . import _lib
     from .comm import shard_walk_range
-    from .distributed import run_protocol
+    from .distributed import run_protocol, solve_key
     from .solvers.WoStSolver import SolveStats, _stats_of_multi
 
     R, rank = int(comm.n_ranks), int(comm.rank)
@@ -477,8 +477,9 @@ def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, rec
                         raise ValueError(f"protocol asked for walks [{a}, {b}), this rank solved [{w0}, {w1})")
                     return blocks
 
+                key = solve_key(group_seed(seed, g), sc.eps, sc.max_steps, sc.points[j0:j1])
                 sums, _, all_steps = run_protocol(R, rank, j1 - j0, int(n_walks), 2 * S + 1, solve_range,
-                                                  comm.allreduce, comm.allgather)
+                                                  comm.allreduce, comm.allgather, key=key)
                 stats = _stats_of_multi(sums, int(n_walks))
                 st = SolveStats(mean=np.stack([x.mean for x in stats]), stderr=np.stack([x.stderr for x in stats]),
                                 mean_steps=stats[0].mean_steps, walks=int(n_walks), total_steps=int(all_steps),

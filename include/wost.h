@@ -30,7 +30,7 @@ typedef unsigned long long uint64_t;
 extern "C" {
 #endif
 
-#define WOST_ABI_VERSION 3
+#define WOST_ABI_VERSION 4
 
 /* Most source fields one multi-source solve can score (wost_set_sources). */
 #define WOST_MAX_SOURCES 16
@@ -338,19 +338,32 @@ int wost_shard_merge(const double* gathered, int64_t n_points, int64_t walks_per
  *   solve_range  this rank's walks [walk_begin, walk_end) of every point ->
  *                blocks [n_points][n_rank_blocks][row] (wost_solve_range's layout)
  *   allreduce    inout[count] reduced over ranks, op WOST_COMM_SUM / WOST_COMM_MAX
- *   allgather    recv[n_ranks][count] = every rank's send[count], in rank order */
+ *   allgather    recv[n_ranks][count] = every rank's send[count], in rank order
+ *   key, n_key   optional (NULL / 0): up to WOST_DIST_MAX_KEY values every rank must
+ *                hold identically -- the solve's other arguments (seed halves, eps,
+ *                maxSteps, a checksum of the points); checked by the agreement */
+#define WOST_DIST_MAX_KEY 16
 typedef struct {
     void* ctx;
     int32_t (*prepare)(void* ctx, int64_t count);
     int32_t (*solve_range)(void* ctx, int64_t walk_begin, int64_t walk_end, double* blocks);
     int32_t (*allreduce)(void* ctx, double* inout, int64_t count, int32_t op);
     int32_t (*allgather)(void* ctx, const double* send, int64_t count, double* recv);
+    const double* key;
+    int32_t n_key;
 } wost_dist_ops;
+
+/* The agreement key wost_solve_distributed uses: {seed low 32 bits, seed high 32 bits,
+ * eps, max_steps, points checksum low / high 32 bits (FNV-1a 64 of the point bytes)}
+ * -> key[6]. Host only. */
+int wost_dist_solve_key(uint64_t seed, float eps, int32_t max_steps, const float* points, int64_t n_points,
+                        double* key);
 
 /* The distributed solve's protocol over a transport (collective). Every rank makes
  * exactly two collective calls, in the same order, whatever fails locally:
- *   1. allreduce(MAX) of (failed, n_points, row, walks_per_point) -- so a rank whose
- *      solve or buffers failed, or whose arguments differ, is known to all;
+ *   1. allreduce(MAX) of (failed, n_points, row, walks_per_point, key) and their
+ *      negatives -- so a rank whose solve or buffers failed, or whose arguments
+ *      differ, is known to all;
  *   2. only if no rank failed and all agree: allgather of the packed blocks,
  *      then wost_shard_merge.
  * A rank that failed returns its own status; the others return WOST_ERR_COMM
@@ -366,6 +379,14 @@ int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank
  * interpreting kernel if that fails. enable = 0 forces the precompiled kernel
  * (also: environment WOST_JIT=0). Both give identical results. */
 int wost_set_jit(wost_handle* h, int32_t enable);
+
+/* compat="fixed" with delta tracking: the corrected screened law moves a walk
+ * ~2/sqrt(sigma_bar) per collision, so a point at Dirichlet distance d needs
+ * ~d^2 sigma_bar / 4 steps. Every solve entry point refuses (WOST_ERR_INVALID_ARG)
+ * when that estimate at the median query point exceeds maxSteps -- the walks would
+ * all end truncated (the DCR configurations: sigma_bar = 10, d ~ 100). enable = 0
+ * turns the check off (default on). No reference counterpart. */
+int wost_set_fixed_step_check(wost_handle* h, int32_t enable);
 
 /* Neumann segment tree: for a Neumann polyline of at least min_segments
  * segments (default WOST_TREE_MIN_SEGMENTS_DEFAULT; < 0: never, 0: always)
@@ -415,13 +436,18 @@ int wost_screened_cdf_fixed(double s, const double* rho, int64_t n, double* cdf)
  *   op 2 silhouetteDistance(:83-102, :255-265)  out_f[n]
  *   op 3 rayIntersection   (:104-132, :281-292) out_f[n][nv-1]  (dirs used)
  *   op 4 intersectPolylines(:134-197, :294-307) out_f[n][5] = x, y, nx, ny, found
- *                                                (dirs and radii used)   */
+ *                                                (dirs and radii used)
+ * op | WOST_GEOM_TREE (ops 2 and 4, >= 2 segments): the same query answered by the
+ * walk kernels' Neumann segment tree (wost_set_segment_tree; default leaf size) one
+ * query per lane instead of the full scan -- bit-identical to the scan, which the
+ * tests check at the reference's own outputs (tests/golden/geometry_kats_c5.npz). */
 enum wost_geom_op {
     WOST_GEOM_DISTANCE = 0,
     WOST_GEOM_IS_SILHOUETTE = 1,
     WOST_GEOM_SILHOUETTE_DISTANCE = 2,
     WOST_GEOM_RAY_INTERSECTION = 3,
-    WOST_GEOM_INTERSECT_POLYLINES = 4
+    WOST_GEOM_INTERSECT_POLYLINES = 4,
+    WOST_GEOM_TREE = 256
 };
 int wost_geometry_query(int32_t device, int32_t op, const wost_polyline* poly,
                         const float* points, const float* dirs, const float* radii,

@@ -123,4 +123,26 @@ int tree_check_nearest(const float* xy, int nv, int leaf, const float* pts, cons
     return 0;
 }
 
+// The tree's raw answers (what wost_geometry_query(op | WOST_GEOM_TREE) returns on the
+// device): silhouette_distance_tree without a Dirichlet bound -> sil[n], and
+// intersect_polylines_tree (reference mode) -> hit[n][5] = x, y, nx, ny, found.
+int tree_query(const float* xy, int nv, int leaf, const float* pts, const float* dirs, const float* radii, long n,
+               float* sil, float* hit) {
+    SegmentTreeHost th;
+    if (!build_segment_tree(xy, nv, leaf, &th)) return 1;
+    const SegTree t{reinterpret_cast<const float4*>(th.rec.data()), reinterpret_cast<const float2*>(xy), nv,
+                    th.first_leaf, th.depth, th.leaf, th.tol, th.kmax};
+    for (long i = 0; i < n; ++i) {
+        const float px = pts[2 * i], py = pts[2 * i + 1];
+        sil[i] = silhouette_distance_tree(t, px, py, WOST_INF);
+        const Hit h = intersect_polylines_tree(t, px, py, dirs[2 * i], dirs[2 * i + 1], radii[i]);
+        hit[5 * i + 0] = h.x;
+        hit[5 * i + 1] = h.y;
+        hit[5 * i + 2] = h.nx;
+        hit[5 * i + 3] = h.ny;
+        hit[5 * i + 4] = h.hit ? 1.f : 0.f;
+    }
+    return 0;
+}
+
 }  // extern "C"

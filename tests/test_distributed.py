@@ -290,6 +290,8 @@ def _protocol_worker(rank, world, port, W, mode, out_q):
     ar, ag = D.torch_transport()
 
     myW = W + 4096 if (mode == "disagree" and rank == 1) else W
+    seed = 100 if (mode == "disagree_seed" and rank == 1) else 99
+    key = D.solve_key(seed, sc.eps, sc.max_steps, pts) if mode.startswith("disagree_") or mode == "ok" else None
 
     def solve_range(w0, w1):
         if mode == "fail" and rank == world - 1:
@@ -297,7 +299,7 @@ def _protocol_worker(rank, world, port, W, mode, out_q):
         return _oracle_range_blocks(sc, pts, myW, w0, w1, 99)
 
     try:
-        sums, rng_, steps = D.run_protocol(world, rank, len(pts), myW, 3, solve_range, ar, ag)
+        sums, rng_, steps = D.run_protocol(world, rank, len(pts), myW, 3, solve_range, ar, ag, key=key)
         res = ("ok", sums, rng_, steps)
     except RuntimeError as e:
         res = (type(e).__name__, str(e), None, None)
@@ -351,11 +353,27 @@ def test_library_protocol_failure_on_one_rank_reaches_every_rank():
     assert res[0][0] == "WostError" and "another rank failed" in res[0][1]
 
 
-def test_library_protocol_rejects_disagreeing_ranks():
-    """Ranks called with different walk counts agree to fail (ValueError on all)."""
-    res = _run_protocol_world(2, 2 * 4096, "disagree")
+@pytest.mark.parametrize("mode", ["disagree", "disagree_seed"])
+def test_library_protocol_rejects_disagreeing_ranks(mode):
+    """Ranks called with different walk counts, or with different arguments in the
+    agreement key (here the seed: wost_dist_solve_key), agree to fail (ValueError on all)."""
+    res = _run_protocol_world(2, 2 * 4096, mode)
     for r in range(2):
         assert res[r][0] == "ValueError" and "disagree" in res[r][1], res[r]
+    if mode == "disagree_seed":
+        assert "arguments" in res[0][1]
+
+
+def test_solve_key_covers_seed_eps_steps_and_points():
+    from dcrmontecarlo_amd import scenarios as S
+
+    pts = S.poisson_square().points[:5]
+    k = D.solve_key(2**40 + 7, 1e-4, 500, pts)
+    assert k[0] == 7 and k[1] == 2**8 and k[2] == np.float32(1e-4) and k[3] == 500
+    p2 = pts.copy()
+    p2[3, 1] = np.nextafter(p2[3, 1], np.float32(9))
+    assert not np.array_equal(k[4:], D.solve_key(2**40 + 7, 1e-4, 500, p2)[4:])
+    assert np.array_equal(k, D.solve_key(2**40 + 7, 1e-4, 500, pts.astype(np.float64)))
 
 
 def test_library_protocol_eight_thread_ranks_with_oracle_shards():

@@ -64,7 +64,9 @@ def test_c5_device_matches_oracle(gpu_available):
     W = 512
     gv, gs = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=31337)
     gv, gs = gv.ravel(), gs.ravel()
-    pb = O.Problem.from_scenario(sc, sigma_bar=s.sigma_bar)
+    sb = O.Problem.from_scenario(sc).sigma_bar()        # the oracle's OWN sigma_bar (gridSampleMinMax restated)
+    assert s.sigma_bar == pytest.approx(sb, rel=1e-5)
+    pb = O.Problem.from_scenario(sc, sigma_bar=sb)
     ov, os_ = pb.solve_walks(pts, W, sc.max_steps, sc.eps, 31337)
     try:
         O.set_direction_perturbation(1.2e-7)       # 1 ulp of the step direction
@@ -125,3 +127,22 @@ def test_c5_wenner_survey_batches_equal_single_source_solves(gpu_available):
             u, st = sm.solve(sc.points[j0:j1], nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=gseed,
                              return_stats=True)
             assert st.mean[q + 1 - j0] - st.mean[q + 2 - j0] == res.model.dv[q]
+
+
+def test_long_tree_with_wide_leaves_steps_down_its_staging(gpu_available):
+    """25,000 segments in leaves of 32 keep the records under the 64-KB
+    staging budget while the Neumann vertices (200 KB) cannot join them in LDS. The
+    host must step down to records-only staging (not build a kernel that reads
+    vertices it never staged); the tree kernel's walks equal the scan kernel's bit for
+    bit."""
+    sc = _c5(n_electrodes=32, n_walks=1, n_segments=25_000)
+    s = sc.solver(device=0)
+    s.set_segment_tree(0, 32)
+    pts = sc.points[::4]
+    tv, ts = s.solve_walks(pts, nWalks=128, maxSteps=sc.max_steps, eps=sc.eps, seed=41)
+    assert s.last_timing["tree"] == 1
+    s.set_segment_tree(-1)
+    bv, bs = s.solve_walks(pts, nWalks=128, maxSteps=sc.max_steps, eps=sc.eps, seed=41)
+    assert s.last_timing["tree"] == 0
+    np.testing.assert_array_equal(ts, bs)
+    np.testing.assert_array_equal(tv.view(np.uint32), bv.view(np.uint32))

@@ -219,3 +219,28 @@ def test_fixed_delta_kernels_are_deterministic_and_agree(gpu_available, case):
     assert b.last_timing["jit"] == 0
     np.testing.assert_array_equal(s0, s2)
     np.testing.assert_array_equal(v0, v2)
+
+
+def test_fixed_delta_refuses_walks_that_would_all_be_truncated(gpu_available):
+    """on the DCR configurations the corrected screened law moves a
+    walk ~2/sqrt(sigma_bar) = 0.6 per collision, ~100 from the Dirichlet box: every walk
+    would end at maxSteps. compat="fixed" refuses such solves (ValueError naming the
+    estimate) in every entry point; with the check off the truncation is plain to see;
+    with enough steps for the estimate the solve runs."""
+    from dcrmontecarlo_amd import scenarios as S
+
+    sc = S.dcr_dipole(n_electrodes=8, n_walks=1)
+    s = sc.solver(device=0, compat="fixed")
+    assert s.sigma_bar == pytest.approx(10.0)
+    for call in (lambda: s.solve(sc.points, nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=1),
+                 lambda: s.solve_walks(sc.points, nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=1),
+                 lambda: s.solve_range(sc.points, 4096, 0, 4096, sc.max_steps, sc.eps, 1)):
+        with pytest.raises(ValueError, match="truncate"):
+            call()
+    s.set_fixed_step_check(False)
+    _, st = s.solve_walks(sc.points, nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=1)
+    assert np.mean(st == sc.max_steps) > 0.99          # what the check prevents
+    # the reference mode on the same problem terminates (the ~76 steps of its rescaled law)
+    r = sc.solver(device=0)
+    _, sr = r.solve_walks(sc.points, nWalks=256, maxSteps=sc.max_steps, eps=sc.eps, seed=1)
+    assert np.mean(sr < sc.max_steps) > 0.99

@@ -96,6 +96,10 @@ def test_fixed_topography_tree_equals_scan(gpu_available):
     a = sc.solver(device=0, compat="fixed")
     b = sc.solver(device=0, compat="fixed")
     b.set_segment_tree(-1)
+    # the literal C5 fields (sigma_bar 0.5, electrodes ~300 from the Dirichlet sides)
+    # would need ~1e4 steps per walk: truncated walks on purpose, for the bit comparison
+    for s in (a, b):
+        s.set_fixed_step_check(False)
     pts = sc.points[::4]
     v0, s0 = a.solve_walks(pts, nWalks=256, maxSteps=200, eps=sc.eps, seed=3)
     v1, s1 = b.solve_walks(pts, nWalks=256, maxSteps=200, eps=sc.eps, seed=3)

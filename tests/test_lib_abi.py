@@ -14,7 +14,7 @@ def test_library_exports_every_declared_symbol():
     assert len(declared) >= 13
     missing = [s for s in declared if not hasattr(_lib.lib, s)]
     assert not missing, missing
-    assert _lib.lib.wost_version() == _lib.ABI_VERSION == 3
+    assert _lib.lib.wost_version() == _lib.ABI_VERSION == 4
 
 
 def test_num_blocks():

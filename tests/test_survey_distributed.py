@@ -129,12 +129,12 @@ def test_distributed_survey_equals_one_rank_with_one_collective_order(R, walks):
             np.testing.assert_array_equal(got.se, want.se)
         assert res[r].walk_steps == one.walk_steps
     # one collective sequence on every rank: per group, model then background, each an
-    # agreement all-reduce (7 numbers) and -- when some rank holds walks -- one all-gather
+    # agreement all-reduce (41 numbers) and -- when some rank holds walks -- one all-gather
     G = len(list(survey.wenner_batches(40, 1)))
     logs = [comms[r].log for r in range(R)]
     assert all(lg == logs[0] for lg in logs)
     ag = [e for e in logs[0] if e[0] == "allreduce"]
-    assert len(ag) == 2 * G and all(e == ("allreduce", "max", 7) for e in ag)
+    assert len(ag) == 2 * G and all(e == ("allreduce", "max", 41) for e in ag)   # wost_distributed_run agreement
     assert sum(e[0] == "allgather" for e in logs[0]) == 2 * G
     sizes = [e[1] for e in logs[0] if e[0] == "allgather"]
     assert sizes[0::2] == sizes[1::2]       # model and background of a group gather alike

@@ -183,6 +183,29 @@ def ref_scenarios():
                     alpha=ns["conductivity_field_torch"])
 
     out["notebook_dcr"] = notebook
+
+    def wenner(physical):
+        """C5: the notebook's cell-17 callables and cell-18 U boundary with the
+        synthetic 10k-segment topography as the Neumann surface. ``physical`` drops cell 17's
+        air term: the remaining lines of conductivity_field_torch, with the reference's own
+        torch_smooth_circle."""
+        nb = json.load(open(os.path.join(REF, "tests", "testNotebook.ipynb")))
+        ns = {"torch": torch, "torch_smooth_circle": torch_smooth_circle, "np": np}
+        exec("".join(nb["cells"][17]["source"]), ns)
+        dp = torch.tensor([[-500.0, 1], [-500.0, -1000.0], [500.0, -1000.0], [500.0, 1]])
+        topo = torch.from_numpy(S.topography(10_000))
+        alpha = ns["conductivity_field_torch"]
+        if physical:
+            def alpha(point):
+                bg = 1e-2
+                a1 = (1e-1 - bg) * torch_smooth_circle(point, torch.tensor([-120, -80]), 60)
+                a2 = (1e-3 - bg) * torch_smooth_circle(point, torch.tensor([120, -80]), 60)
+                return bg + a1 + a2
+        return dict(D=RefPoly(dp), N=RefPoly(topo), g=lambda p: 0.0, f=ns["dcr_current_source_torch"], sigma=None,
+                    alpha=alpha)
+
+    out["wenner_topography"] = lambda: wenner(False)
+    out["wenner_topography_physical"] = lambda: wenner(True)
     return out
 
 
@@ -250,17 +273,81 @@ def gen_geometry():
     print("geometry_kats.npz", len(geoms), "geometries")
 
 
-def gen_fields():
+def _ref_queries(V, P, Dd, R):
+    """The five PolyLinesSimple queries of the reference at each (point, direction, radius)."""
+    poly = RefPoly(torch.from_numpy(V))
+    dist, sil, sild, ray, ip = [], [], [], [], []
+    for q in range(len(P)):
+        p = torch.from_numpy(P[q])
+        d = torch.from_numpy(Dd[q])
+        dist.append(float(poly.distance(p)))
+        sil.append(poly.isSilhouette(p).numpy().astype(np.uint8))
+        sild.append(float(poly.silhouetteDistance(p)))
+        ray.append(poly.rayIntersection(p, d).numpy())
+        xp, nrm, found = poly.intersectPolylines(p, d, float(R[q]))
+        ip.append(np.concatenate([xp.numpy(), nrm.numpy().astype(np.float32), [np.float32(bool(found))]]))
+    nq = len(P)
+    return {"distance": np.array(dist, np.float32),
+            "is_silhouette": np.array(sil, np.uint8).reshape(nq, max(len(V) - 2, 0)),
+            "silhouette_distance": np.array(sild, np.float32),
+            "ray_intersection": np.array(ray, np.float32).reshape(nq, len(V) - 1),
+            "intersect": np.array(ip, np.float32)}
+
+
+def gen_c5_kats(n=320):
+    """G1 for C5 where its walks actually query the surface: the reference's five queries on
+    the 10k-segment topography at n positions drawn from recorded C5 walks
+    (tests/golden/c5_walk_positions.npz, those within 4 units of the surface first), with
+    random unit directions and radii of the walks' own scale (the Dirichlet distance there).
+    The segment tree must return these bit for bit."""
+    rng = np.random.default_rng(505)
+    V = S.topography(10_000)
+    z = np.load(os.path.join(OUT, "c5_walk_positions.npz"))
+    P0, dd = z["points"], z["dd"]
+    near = np.abs(P0[:, 1] - (1.0 + 2.0 * np.sin(P0[:, 0].astype(np.float64) / 37.0))) < 4.0
+    idx = np.concatenate([rng.choice(np.flatnonzero(near), n * 3 // 4, replace=False),
+                          rng.choice(np.flatnonzero(~near), n - n * 3 // 4, replace=False)])
+    P = np.ascontiguousarray(P0[idx], np.float32)
+    th = rng.random(n) * 2 * np.pi
+    Dd = np.stack([np.cos(th), np.sin(th)], 1).astype(np.float32)
+    R = np.maximum(dd[idx], 0.5).astype(np.float32) * (0.5 + rng.random(n)).astype(np.float32)
+    out = {"topo10k_walk__verts": V, "topo10k_walk__points": P, "topo10k_walk__dirs": Dd,
+           "topo10k_walk__radii": R.astype(np.float32)}
+    for k, v in _ref_queries(V, P, Dd, R).items():
+        out[f"topo10k_walk__{k}"] = v
+    np.savez_compressed(os.path.join(OUT, "geometry_kats_c5.npz"), **out)
+    print("geometry_kats_c5.npz", n, "points,", int(near[idx].sum()), "near the surface,",
+          int(out["topo10k_walk__intersect"][:, 4].sum()), "ray hits,",
+          int(np.isfinite(out["topo10k_walk__silhouette_distance"]).sum()), "finite silhouettes")
+
+
+FIELD_SCENARIOS = ["laplace_square", "manufactured_polynomial", "poisson_square", "variable_coefficients",
+                   "dcr_dipole", "notebook_dcr"]
+C5_SCENARIOS = ["wenner_topography", "wenner_topography_physical"]
+
+
+def gen_fields(names=None):
     specs = ref_scenarios()
-    rng = np.random.default_rng(11)
-    for name in ["laplace_square", "manufactured_polynomial", "poisson_square", "variable_coefficients",
-                 "dcr_dipole", "notebook_dcr"]:
+    for k, name in enumerate(names or FIELD_SCENARIOS):
+        # one generator per scenario, seeded as the six original ones were drawn in
+        # sequence from rng(11): regenerating a subset leaves the others' points as they are
+        rng = np.random.default_rng(11)
+        for _ in range(FIELD_SCENARIOS.index(name) if name in FIELD_SCENARIOS else 0):
+            rng.random((256, 2))
+        if name in C5_SCENARIOS:
+            rng = np.random.default_rng(1100 + C5_SCENARIOS.index(name))
         spec = specs[name]()
         V = spec["D"].points.numpy()
         if spec["N"] is not None:
             V = np.concatenate([V, spec["N"].points.numpy()])
         lo, hi = V.min(0), V.max(0)
         P = (lo + rng.random((256, 2)) * (hi - lo)).astype(np.float32)
+        if name in C5_SCENARIOS:
+            # half of them where the walks live: within 4 units of the topography
+            # (the electrodes sit 0.1 below it; the literal air term switches at y = 0)
+            x = (lo[0] + rng.random(128) * (hi[0] - lo[0])).astype(np.float32)
+            y = (1.0 + 2.0 * np.sin(x.astype(np.float64) / 37.0) - rng.random(128) * 4.0).astype(np.float32)
+            P[:128] = np.stack([x, y], 1)
         res = {"points": P, "dirichlet": spec["D"].points.numpy().astype(np.float32)}
         if spec["N"] is not None:
             res["neumann"] = spec["N"].points.numpy().astype(np.float32)
@@ -432,6 +519,11 @@ REPLAYS = {
     # electrodes next to the +-10 m current sources (x = -10.5, -7.5, 7.5, 10.5)
     "dcr_dipole": lambda: (S.dcr_dipole().points[[20, 21, 26, 27]], 16, 500, 0.9, 2024),
     "notebook_dcr": lambda: (S.notebook_dcr().points[[4, 5, 15, 16]], 8, 500, 0.9, 5),
+    # C5: eight electrodes along the line, four of them next to the notebook source's +-200 m
+    # poles (x = -202.5, -193.1, 193.1, 202.5), on the 10k-segment topography (each step of the
+    # reference scans all 10k segments twice: ~1.6 ms per step)
+    "wenner_topography": lambda: (S.wenner_topography(n_walks=1).points[[31, 63, 66, 100, 156, 189, 192, 224]], 32, 500,
+                                  0.9, 77),
 }
 
 
@@ -633,11 +725,15 @@ def main():
         gen_geometry()
     if "fields" in parts:
         gen_fields()
+    if "c5_fields" in parts:
+        gen_fields(C5_SCENARIOS)
+    if "c5_kats" in parts:
+        gen_c5_kats()
     if "greens" in parts:
         gen_greens()
     if "sampler" in parts:
         gen_sampler_draws()
-    names = a.scenarios.split(",") if a.scenarios else list(REPLAYS)
+    names = a.scenarios.split(",") if a.scenarios else [n for n in REPLAYS if n != "wenner_topography"]
     if "replay" in parts:
         gen_replays(names)
     if "stats" in parts:

@@ -71,6 +71,8 @@ def main():
         W = max(1, int(W * a.scale))
         sc = S.ALL[name]()
         solver = sc.solver(device=int(os.environ.get("LOCAL_RANK", "0")), compat=a.compat)
+        if a.compat == "fixed":   # timing of truncated walks is still timing (the DCR configs)
+            solver.set_fixed_step_check(False)
         if a.scan:
             solver.set_segment_tree(-1)
         pts = sc.points[:npts]
