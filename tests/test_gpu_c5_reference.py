@@ -9,7 +9,8 @@ tests/test_c5_reference.py for the fixtures and the tolerances' origin):
 * the reference's C5 walks replayed on the Philox stream (8 electrodes x 32 walks):
   the device's walks (tree kernel, field-specialised) agree at least as often as the
   oracle agrees with itself under a 1-ulp change of the step direction, less 2 points,
-  and every walk value is within 1e-4 for >= 95% of the walks.
+  >= 95% of the walk values are within 1e-4, and the per-electrode means agree within
+  3 combined standard errors.
 """
 import numpy as np
 import pytest
@@ -97,6 +98,10 @@ def test_c5_device_replays_reference_walks(gpu_available):
     chaos = float(((ps == os_) & (np.abs(pv - ov) <= 1e-3 * np.abs(ov) + 1e-5 * scale)).mean())
     assert same >= chaos - 0.02, (same, chaos)
     assert close >= 0.95, close
+    # per-electrode means within 3 combined standard errors: a walk that diverged (chaos)
+    # carries a heavy-tailed value of the literal fields, so exact means are not expected
     n = len(z["points"])
-    np.testing.assert_allclose(v.astype(np.float64).reshape(n, -1).mean(1), z["walk_values"].reshape(n, -1).mean(1),
-                               rtol=1e-3, atol=1e-6 * np.abs(z["walk_values"]).max())
+    g = v.astype(np.float64).reshape(n, -1)
+    r = z["walk_values"].reshape(n, -1)
+    se = np.sqrt(g.var(1, ddof=1) / W + r.var(1, ddof=1) / W)
+    assert np.all(np.abs(g.mean(1) - r.mean(1)) <= 3.0 * se + 1e-9 * np.abs(r).max()), (g.mean(1), r.mean(1), se)

@@ -179,10 +179,11 @@ def test_multi_source_shards_merge_through_the_protocol(gpu_available):
 
 
 def test_wenner_survey_through_communicators_equals_one_gpu(gpu_available):
-    """The C5 survey's multi-GPU path (survey.run_wenner_survey(comm=...), every group
-    through comm.solve_sources_distributed) on one-rank RCCL communicators -- one shared
-    by both fields, and a (model, background) pair -- equals the one-GPU survey bit
-    for bit (reduced: 24 electrodes, 2,000-segment topography)."""
+    """The C5 survey's multi-GPU path (survey.run_wenner_survey(comm=...): both fields'
+    walk-range solves concurrent, every collective of libwost's protocol issued from
+    one thread in a fixed order) on a one-rank RCCL communicator equals the one-GPU
+    survey bit for bit (reduced: 24 electrodes, 2,000-segment topography), with the
+    fields concurrent or not; a communicator pair is refused."""
     from dcrmontecarlo_amd import comm
     from dcrmontecarlo_amd import scenarios as S
     from dcrmontecarlo_amd import survey
@@ -193,12 +194,15 @@ def test_wenner_survey_through_communicators_equals_one_gpu(gpu_available):
     ref = survey.run_wenner_survey(sc, 1e-2, sc.n_walks, seed=3, solvers=(sm, sh), concurrent=False)
     cs = [comm.Communicator(comm.unique_id(), 1, 0, 0) for _ in range(2)]
     try:
-        for cm in (cs[0], (cs[0], cs[1])):
-            got = survey.run_wenner_survey(sc, 1e-2, sc.n_walks, seed=3, solvers=(sm, sh), comm=cm)
+        for concurrent in (True, False):
+            got = survey.run_wenner_survey(sc, 1e-2, sc.n_walks, seed=3, solvers=(sm, sh), comm=cs[0],
+                                           concurrent=concurrent)
             for a, b in ((got.model, ref.model), (got.background, ref.background)):
                 assert np.array_equal(a.dv, b.dv) and np.array_equal(a.se, b.se)
             assert np.array_equal(got.rho.rho_a, ref.rho.rho_a, equal_nan=True)
             assert got.walk_steps == got.local_walk_steps == ref.walk_steps
+        with pytest.raises(ValueError, match="one communicator"):
+            survey.run_wenner_survey(sc, 1e-2, sc.n_walks, seed=3, solvers=(sm, sh), comm=(cs[0], cs[1]))
     finally:
         for c in cs:
             c.close()

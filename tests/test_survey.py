@@ -175,13 +175,9 @@ class _FakeSolver:
 
 
 @pytest.mark.parametrize("E,a", [(40, 1), (23, 2)])
-def test_wenner_survey_bookkeeping_one_gpu_and_communicator(E, a, monkeypatch):
+def test_wenner_survey_bookkeeping_one_gpu(E, a):
     """run_wenner_survey on host stand-ins: every quadripole's dV is u_q(M) - u_q(N) of
-    its own transmitter, each group is solved once per field with its own seed, and the
-    communicator path (comm.solve_sources_distributed; one communicator or a pair) fills
-    the same tables and counts the ranks' walk-steps."""
-    from dcrmontecarlo_amd import comm as C
-
+    its own transmitter, and each group is solved once per field with its own seed."""
     sc = S.wenner_topography(n_electrodes=E, n_walks=8, n_segments=100)
     Q = E - 3 * a
     srcs = [survey.dipole_source(sc.points[q], sc.points[q + 3 * a], 0.5) for q in range(Q)]
@@ -198,21 +194,8 @@ def test_wenner_survey_bookkeeping_one_gpu_and_communicator(E, a, monkeypatch):
     np.testing.assert_allclose(r1.rho.rho_a, 1e2 * 2.0)
     assert r1.walk_steps == r1.local_walk_steps == 2 * E * 8
 
-    def fake_dist(solver, comm, pts, sources, nWalks, maxSteps, eps, seed=0):
-        u, st = solver.solve_sources(pts, sources, nWalks, maxSteps, eps, seed, True)
-        st.total_steps *= comm.n_ranks
-        return u, st, {"total_steps": st.total_steps // comm.n_ranks}
-
-    monkeypatch.setattr(C, "solve_sources_distributed", fake_dist)
-
-    class _Comm:
-        n_ranks = 4
-
-    for comm in (_Comm(), (_Comm(), _Comm())):
-        fm.calls.clear()
-        r2 = survey.run_wenner_survey(sc, 1e-2, 8, a=a, seed=3, solvers=(fm, fh), comm=comm)
-        assert np.array_equal(r2.model.dv, r1.model.dv) and np.array_equal(r2.background.dv, r1.background.dv)
-        assert r2.walk_steps == 4 * r2.local_walk_steps == 4 * r1.walk_steps
+    # the communicator path (walk-range shards, one fixed collective order) runs the real
+    # protocol over thread ranks in tests/test_survey_distributed.py
 
 
 def test_apparent_resistivity_resolves_only_with_the_model_error_small():
