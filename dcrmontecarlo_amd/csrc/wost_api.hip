@@ -1189,9 +1189,19 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
         const float2 n = segment_left_normal(a, b);
         phi[i] = std::atan2(n.y, n.x);
     }
+    // offline study of the tree kernels' LDS staging (tools/jit_isa.py --stage): the source
+    // of staging level WOST_KERNEL_SOURCE_STAGE (2: records and vertices, 1: records, with
+    // WOST_TREE_LDS_BLOCK's workgroup) instead of the 256-thread unstaged kernel
+    int stage = 0, block = kWalkBlock;
+    if (const char* e = std::getenv("WOST_KERNEL_SOURCE_STAGE"); e && mode_tree(mode)) {
+        stage = std::max(0, std::min(2, std::atoi(e)));
+        block = stage == 2 ? kTreeStageVertsBlock : stage == 1 ? kTreeStageBlock : kWalkBlock;
+        if (const char* b = std::getenv("WOST_TREE_LDS_BLOCK"); b && stage == 1)
+            block = std::max(64, std::min(1024, std::atoi(b) / 64 * 64));
+    }
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
-                                         (int)(h->dverts.size() / 2), h->nverts.data(), nn, false, 1, kWalkBlock,
-                                         phi.empty() ? nullptr : phi.data());
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), nn, false, 1, block,
+                                         phi.empty() ? nullptr : phi.data(), false, stage);
     delete h;
     *length = (int64_t)src.size();
     if (out && capacity > 0) {
