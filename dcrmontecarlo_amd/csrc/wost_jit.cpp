@@ -402,6 +402,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
+    if (const char* e = std::getenv("WOST_JIT_PHILOX_AHEAD"))   // A/B: Philox one step ahead
+        o << "#define WOST_PHILOX_AHEAD " << std::max(0, std::min(3, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_REFILL_MIN"))   // A/B: refill batch size
         o << "#define WOST_REFILL_MIN " << std::max(1, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE"))   // A/B: tree hand-out threshold (0: none)

@@ -645,6 +645,21 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
 #ifndef WOST_REFILL_MIN   // idle lanes that trigger a refill (tools/ab_refill.sh; 1 = every iteration)
 #define WOST_REFILL_MIN 4
 #endif
+// Philox one step ahead: step k's random words are drawn during step k - 1 (at the
+// refill for step 0), right after that step's direction, where the ten dependent
+// multiply rounds can overlap the step's geometry and field arithmetic instead of
+// heading the next step's dependency chain. The words depend only on (seed, walk id,
+// step), so the bits are unchanged.
+// (1: where the compiler puts it -- it sinks the draw to the loop latch; 2: pinned
+// right after the direction; 3: pinned before the source sample's clip test)
+#ifndef WOST_PHILOX_AHEAD
+#define WOST_PHILOX_AHEAD 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define WOST_PIN_U4(u) __asm__ volatile("" : "+v"((u).x), "+v"((u).y), "+v"((u).z), "+v"((u).w))
+#else
+#define WOST_PIN_U4(u) ((void)0)
+#endif
 template <bool NEU, bool SRC, bool DELTA, bool TREE, bool REC, int NS = 1, bool FIX = false, bool GL = false,
           class F>
 __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsigned char* smem) {
@@ -726,6 +741,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     float phi = 0.f;            // atan2 of currentNormal (:228), set when onB
     float w = 1.f;              // attenuation_coef
     float ax = 1.f;             // alpha(current_point), cached
+    U4 rn_ahead{0u, 0u, 0u, 0u};   // (WOST_PHILOX_AHEAD) the words of this walk's step k
     float total[NS];            // this walk's contributions (one per source)
 #pragma unroll
     for (int s = 0; s < NS; ++s) total[s] = 0.f;
@@ -814,6 +830,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                     else if (rem >= A.walks_per_point) ++pid;
                 }
                 pw = philox_walk(wid, A.key0, A.key1);
+                if (WOST_PHILOX_AHEAD) rn_ahead = philox_draw(pw, 0u, A.key0, A.key1);
                 const float2 q = A.points[pid];
                 px = q.x; py = q.y;
                 k = 0; dD = FIX ? WOST_INF : 1.0f; onB = false; phi = 0.f; w = 1.f;
@@ -853,10 +870,14 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             // the key enters each step opaque, so its round schedule (key + r * W) is
             // formed by scalar adds here instead of 16 loop-invariant SGPRs, which the
             // register allocator would otherwise spill to VGPR lanes (a v_readlane each)
-            uint32_t key0 = A.key0, key1 = A.key1;
-            WOST_OPAQUE_SGPR(key0);
-            WOST_OPAQUE_SGPR(key1);
-            rn = philox_draw(pw, (uint32_t)k, key0, key1);           // philox4x32_10({k, 0, wid})
+            if (WOST_PHILOX_AHEAD) {
+                rn = rn_ahead;                                       // drawn during the previous step
+            } else {
+                uint32_t key0 = A.key0, key1 = A.key1;
+                WOST_OPAQUE_SGPR(key0);
+                WOST_OPAQUE_SGPR(key1);
+                rn = philox_draw(pw, (uint32_t)k, key0, key1);       // philox4x32_10({k, 0, wid})
+            }
 #endif
             float theta = (u01(rn.x) * 2.0f) * kPiF;                 // :226
             // :227-228 (quirk Q2): atan2(normal) is a property of the segment that
@@ -884,6 +905,15 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             r = dd > A.rmin ? dd : A.rmin;                           // :215
         }
         draw_direction();
+#if !defined(WOST_ABL_NO_PHILOX)
+        if (WOST_PHILOX_AHEAD) {   // the next step's words, overlapping this step's arithmetic
+            uint32_t key0 = A.key0, key1 = A.key1;
+            WOST_OPAQUE_SGPR(key0);
+            WOST_OPAQUE_SGPR(key1);
+            rn_ahead = philox_draw(pw, (uint32_t)(k + 1), key0, key1);
+            if (WOST_PHILOX_AHEAD == 2) WOST_PIN_U4(rn_ahead);
+        }
+#endif
 
         float xnx, xny;
         if (NEU) {                                                   // :235-236
@@ -942,6 +972,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 // needs a2 > b2 (rare: only Neumann hits make the next point closer);
                 // only then evaluate the reference's exact comparison.
                 const float a2 = e1x * e1x + e1y * e1y, b2 = e2x * e2x + e2y * e2y;
+                if (WOST_PHILOX_AHEAD == 3) WOST_PIN_U4(rn_ahead);
                 // a real branch (the compiler otherwise evaluates both correctly rounded
                 // square roots for every lane and selects, ~35 instructions per step)
                 if (WOST_ANY(a2 > b2)) {
