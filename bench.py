@@ -304,6 +304,12 @@ def launch_ranks(n: int, argv: list[str]) -> int:
                 procs[q].wait()
 
     live = set(range(n))
+
+    def on_term(signum, frame):   # a launcher stopping this parent stops the ranks too
+        stop(sorted(q for q in range(n) if procs[q].poll() is None))
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
     try:
         while live:
             failed = None

@@ -84,7 +84,7 @@ class SocketStore:
 
     def __init__(self, host: str, port: int, is_master: bool, timeout: float = 300.0):
         self.timeout = float(timeout)
-        self._srv = None
+        self._srv = self._f = self._sock = None
         if is_master:
             self.kv, self.cond, self.closed = {}, threading.Condition(), False
             self._srv = _StoreServer(("", int(port)), _StoreHandler)
@@ -123,11 +123,14 @@ class SocketStore:
 
     def close(self):
         try:
-            self._f.close()
-            self._sock.close()
+            if getattr(self, "_f", None) is not None:
+                self._f.close()
+            if getattr(self, "_sock", None) is not None:
+                self._sock.close()
         except OSError:
             pass
-        if self._srv is not None:
+        self._f = self._sock = None
+        if getattr(self, "_srv", None) is not None:
             with self.cond:
                 self.closed = True
                 self.cond.notify_all()
@@ -140,12 +143,19 @@ class SocketStore:
 
 class _FileStore:
     """Rank 0 publishes the id in a file named after the ranks' common parent process
-    (torchrun's agent on this node) and the launch's port, the others wait for it; the
+    (torchrun's agent on this node) and the launch's port, in a directory private to
+    this user, and the others wait for it; the
     file is removed when rank 0's communicator closes (every rank has read it by then:
     ncclCommInitRank is collective)."""
 
     def __init__(self, tag: str, rank: int, timeout: float):
-        self.dir, self.tag, self.rank, self.timeout, self.paths = tempfile.gettempdir(), tag, rank, timeout, []
+        # a directory only this user can write, so no other user can plant an id there
+        d = os.path.join(tempfile.gettempdir(), f"wost-{os.getuid()}")
+        os.makedirs(d, mode=0o700, exist_ok=True)
+        st = os.stat(d)
+        if st.st_uid != os.getuid() or (st.st_mode & 0o022):
+            raise PermissionError(f"{d} is not a private directory of this user")
+        self.dir, self.tag, self.rank, self.timeout, self.paths = d, tag, rank, timeout, []
 
     def _path(self, key: str) -> str:
         safe = "".join(c if c.isalnum() else "_" for c in key)
