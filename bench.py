@@ -261,7 +261,8 @@ def issue_line(perfmodel, kernel_steps_per_s: float, workload: str = "dcr_dipole
             pmc = json.load(f)
     except (OSError, ValueError):
         return None
-    out = perfmodel.issue_fraction(pmc["valu_per_wave_step"], pmc["trans_per_wave_step"], kernel_steps_per_s)
+    out = perfmodel.issue_fraction(pmc["valu_per_wave_step"], pmc["trans_per_wave_step"], kernel_steps_per_s,
+                                   perfmodel.PHILOX_MAD64_PER_STEP)
     out.update({"valu_per_wave_step": pmc["valu_per_wave_step"], "trans_per_wave_step": pmc["trans_per_wave_step"],
                 "pmc_source": pmc.get("source")})
     return out
@@ -666,7 +667,8 @@ def wenner_main(args, world, rank, local):
             # at the tree kernel's rate on one chip-filling launch (the survey's summed kernel
             # times double-count its two concurrent fields)
             rate = out.get("speedup_vs_bruteforce", {}).get("tree_kernel_walk_steps_per_s") or kernel_rate
-            roof.update(perfmodel.issue_fraction(pmc["valu_per_wave_step"], pmc["trans_per_wave_step"], rate))
+            roof.update(perfmodel.issue_fraction(pmc["valu_per_wave_step"], pmc["trans_per_wave_step"], rate,
+                                                 perfmodel.PHILOX_MAD64_PER_STEP))
             roof["walk_steps_per_s"] = rate
             roof.update({"achieved": roof["achieved_simd_cycles_per_s"], "peak": roof["peak_simd_cycles_per_s"],
                          "lane_utilisation": pmc.get("lane_utilisation"), "pmc_source": pmc.get("source")})

@@ -99,16 +99,32 @@ def executed_flops_per_step(scenario) -> float:
     return f - I0E_FLOPS if delta else f
 
 
-def issue_fraction(valu_per_wave_step: float, trans_per_wave_step: float, steps_per_s: float) -> dict:
+# v_mad_u64_u32 (Philox's 32x32 -> 64-bit products) issues in ~7.1 SIMD cycles, not 2:
+# 9.66 cycles with its xor against 2.56 for v_fma_f32 (profiles/r02_fields/isa_rates.log,
+# tools/microbench/isa_rates.hip). A walk-step draws one Philox4x32-10 block: 18 of them
+# (rounds 0-1 hoisted per walk, tests/test_philox_split.py), counted statically.
+MAD64_ISSUE_CYC = 7.1
+PHILOX_MAD64_PER_STEP = 18
+
+
+def issue_fraction(valu_per_wave_step: float, trans_per_wave_step: float, steps_per_s: float,
+                   mad64_per_wave_step: float = 0.0) -> dict:
     """VALU issue-rate roofline: the SIMD cycles one wave-step's instructions occupy,
     (VALU - TRANS) x 2 + TRANS x 8, times the wave-steps per second, over the chip's
-    SIMD cycles per second."""
+    SIMD cycles per second. With mad64_per_wave_step, also the same line with those
+    v_mad_u64_u32 at their measured cost (frac_mad64_measured)."""
     cyc = (valu_per_wave_step - trans_per_wave_step) * VALU_ISSUE_CYC + trans_per_wave_step * TRANS_ISSUE_CYC
     avail = N_SIMDS * CLOCK_GHZ * 1e9
     used = cyc * steps_per_s / 64.0
-    return {"bound": "valu-issue", "cycles_per_wave_step": cyc, "achieved_simd_cycles_per_s": used,
-            "peak_simd_cycles_per_s": avail, "frac": used / avail,
-            "ceiling_walk_steps_per_s": avail * 64.0 / cyc if cyc > 0 else None}
+    out = {"bound": "valu-issue", "cycles_per_wave_step": cyc, "achieved_simd_cycles_per_s": used,
+           "peak_simd_cycles_per_s": avail, "frac": used / avail,
+           "ceiling_walk_steps_per_s": avail * 64.0 / cyc if cyc > 0 else None}
+    if mad64_per_wave_step:
+        cyc2 = cyc + mad64_per_wave_step * (MAD64_ISSUE_CYC - VALU_ISSUE_CYC)
+        out.update({"mad64_per_wave_step": mad64_per_wave_step, "mad64_issue_cycles": MAD64_ISSUE_CYC,
+                    "cycles_per_wave_step_mad64_measured": cyc2,
+                    "frac_mad64_measured": cyc2 * steps_per_s / 64.0 / avail})
+    return out
 
 
 def hbm_bytes_per_walk() -> float:
