@@ -839,6 +839,11 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     int block = kWalkBlock, tree_verts = 0;
     int tree_level = kTreeLdsDefaultLevel;
     int tree_lds = h->jit_enabled ? tree_lds_records(h, mode, tree_level, &block, &tree_verts) : 0;
+    // A/B knob: the workgroup of the field-specialised scan kernels (WOST_WALK_BLOCK, a multiple
+    // of 64 up to 1024): larger workgroups share one LDS copy of the sampler and G_norm tables,
+    // so more waves fit a CU than 256-thread workgroups allow (results are the same bits)
+    if (h->jit_enabled && !mode_tree(mode))
+        if (const char* e = std::getenv("WOST_WALK_BLOCK")) block = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
     const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
     // polylines whose LDS copy would cost the walk kernel its occupancy are read from
     // global memory instead (field-specialised kernels; the precompiled ones stage them)
