@@ -64,6 +64,8 @@ def parse():
                          "C5; the timed survey) or without it (physical); the rho_a report always comes from "
                          "a physical survey")
     ap.add_argument("--no-bruteforce", action="store_true", help="wenner_topography: skip the scan-kernel leg")
+    ap.add_argument("--handle-pairs", type=int, default=1,
+                    help="wenner_topography: (model, background) solver pairs, one host thread and HIP stream each")
     ap.add_argument("--electrodes", type=int, default=None,
                     help="dcr_dipole 48, wenner_topography 256, variable_coefficients 256 (query points)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
@@ -583,6 +585,11 @@ def wenner_main(args, world, rank, local):
     sc = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=args.fields == "physical")
     sm = sc.solver(device=local)
     sh = survey.homogeneous_solver(sc, WENNER_ALPHA_BG, sm, device=local)
+    # (model, background) handle pairs: each its own HIP stream, so 2 x pairs launches share the GPU
+    pairs = [sm, sh]
+    for _ in range(max(1, args.handle_pairs) - 1):
+        m2 = sc.solver(device=local)
+        pairs += [m2, survey.homogeneous_solver(sc, WENNER_ALPHA_BG, m2, device=local)]
     comm = None
     if world > 1 or os.environ.get("WOST_BENCH_FORCE_COMM"):
         comm = C.Communicator.from_env(device=local)
@@ -590,7 +597,7 @@ def wenner_main(args, world, rank, local):
     w0, w1 = C.shard_walk_range(Wt, world, rank)
 
     def step(seed, walks=Wt):
-        return survey.run_wenner_survey(sc, WENNER_ALPHA_BG, walks, seed=seed, solvers=(sm, sh), comm=comm)
+        return survey.run_wenner_survey(sc, WENNER_ALPHA_BG, walks, seed=seed, solvers=tuple(pairs), comm=comm)
 
     def barrier():
         if comm is not None:
@@ -631,6 +638,7 @@ def wenner_main(args, world, rank, local):
                        "electrodes": E, "quadripoles": int(len(res.quadripoles)),
                        "walks_per_electrode": Wt, "walks_per_electrode_per_gpu": w1 - w0,
                        "launches_per_field": res.launches, "walk_steps_per_survey": steps_all // max(args.steps, 1),
+                       "handle_pairs": len(pairs) // 2,
                        "parallelism": (f"walk-range shards of every electrode over {world} GPUs "
                                        "(libwost's protocol over its RCCL communicator, all-gather of block sums; "
                                        "both fields' collectives in a fixed order)") if world > 1 else "one GPU"},

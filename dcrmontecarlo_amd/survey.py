@@ -419,9 +419,10 @@ def group_seed(seed: int, g: int) -> int:
 
 def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent=True):
     """The model and background fields of a multi-source survey across the ranks of one
-    communicator. Worker threads (one per field, or one for both without ``concurrent``)
-    solve this rank's walk range of every group (WostSolver_2D.solve_range with the
-    group's sources installed) and hand the block rows over; THIS thread then runs
+    communicator. Worker threads (one per field and handle pair, or one per handle pair
+    without ``concurrent``) solve this rank's walk range of every group
+    (WostSolver_2D.solve_range with the group's sources installed) and hand the block
+    rows over; THIS thread then runs
     libwost's protocol (distributed.run_protocol: agreement all-reduce, all-gather,
     ordered merge) for group 0 model, group 0 background, group 1 model, ... -- the same
     collective sequence on every rank, whatever the threads' timing. A local failure
@@ -440,28 +441,31 @@ def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, rec
     slots = [[queue.Queue(maxsize=1) for _ in range(G)] for _ in range(2)]
     stop = threading.Event()
 
-    def local(fields):
-        for g, (j0, j1, t0, t1) in enumerate(batches):
-            for f in fields:
-                if stop.is_set():
-                    slots[f][g].put((None, RuntimeError("survey stopped"), None))
-                    continue
-                s = solvers[f]
-                try:
-                    if len(srcs[t0:t1]) > _lib.WOST_MAX_SOURCES:
-                        raise ValueError(f"group {g} needs {t1 - t0} sources (> {_lib.WOST_MAX_SOURCES})")
-                    blocks, tm = None, {"total_steps": 0, "walk_kernel_ms": 0.0, "total_ms": 0.0}
-                    if w1 > w0:
-                        with s.sources_installed(s.source_fields(srcs[t0:t1])):
-                            blocks = s.solve_range(sc.points[j0:j1], int(n_walks), w0, w1, sc.max_steps, sc.eps,
-                                                   group_seed(seed, g))
-                            tm = s.last_timing
-                    slots[f][g].put((blocks, None, tm))
-                except Exception as e:   # noqa: BLE001 -- reported through the protocol
-                    slots[f][g].put((None, e, None))
+    def local(tasks, k):
+        for f, g in tasks:
+            j0, j1, t0, t1 = batches[g]
+            if stop.is_set():
+                slots[f][g].put((None, RuntimeError("survey stopped"), None))
+                continue
+            s = solvers[2 * (g % k) + f]
+            try:
+                if len(srcs[t0:t1]) > _lib.WOST_MAX_SOURCES:
+                    raise ValueError(f"group {g} needs {t1 - t0} sources (> {_lib.WOST_MAX_SOURCES})")
+                blocks, tm = None, {"total_steps": 0, "walk_kernel_ms": 0.0, "total_ms": 0.0}
+                if w1 > w0:
+                    with s.sources_installed(s.source_fields(srcs[t0:t1])):
+                        blocks = s.solve_range(sc.points[j0:j1], int(n_walks), w0, w1, sc.max_steps, sc.eps,
+                                               group_seed(seed, g))
+                        tm = s.last_timing
+                slots[f][g].put((blocks, None, tm))
+            except Exception as e:   # noqa: BLE001 -- reported through the protocol
+                slots[f][g].put((None, e, None))
 
-    groups = [(0,), (1,)] if concurrent else [(0, 1)]
-    threads = [threading.Thread(target=local, args=(fs,), daemon=True) for fs in groups]
+    k = max(1, len(solvers) // 2)   # handles per field: worker (f, w) solves the groups g = w mod k
+    work = [[(f, g) for g in range(G) if g % k == w for f in (0, 1)] for w in range(k)]
+    if concurrent:
+        work = [[(f, g) for (f, g) in wl if f == ff] for wl in work for ff in (0, 1)]
+    threads = [threading.Thread(target=local, args=(wl, k), daemon=True) for wl in work]
     for t in threads:
         t.start()
     try:
@@ -504,7 +508,10 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
     With ``concurrent`` the model and background fields run in two host threads, each on
     its own solver handle and HIP stream (libwost's calls release the GIL), so that two
     launches share the GPU: a group's launch (<= 16 electrodes) under-fills it at small
-    walk counts. The results do not depend on it.
+    walk counts, and its last walks run while the other launch fills the CUs.
+    ``solvers`` may hold several (model, background) handle pairs; group g then runs on
+    pair g mod k, one thread per handle, so that 2k launches share the GPU. The results
+    do not depend on either.
 
     ``comm`` (collective; every rank calls with the same arguments): a
     dcrmontecarlo_amd.comm.Communicator (or any object with its ``n_ranks``, ``rank``,
@@ -528,17 +535,28 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
     batches = list(wenner_batches(E, a))
     acc = [[0, 0.0, 0], [0, 0.0, 0]]   # per field: walk-steps (all ranks), walk-kernel ms, walk-steps (this rank)
 
+    import threading
+
+    lock = threading.Lock()
+    if len(solvers) < 2 or len(solvers) % 2:
+        raise ValueError("solvers: (model, background) handle pairs, e.g. (model, background) or "
+                         "(model, background, model2, background2)")
+    k = len(solvers) // 2   # handle pairs: group g runs on pair g mod k
+
     def record(f, g, st, local):
         j0, j1, t0, t1 = batches[g]
-        mean[f][t0:t1, j0:j1] = st.mean
-        se[f][t0:t1, j0:j1] = st.stderr
-        acc[f][0] += st.total_steps
-        acc[f][1] += st.kernel_ms
-        acc[f][2] += local
+        with lock:
+            mean[f][t0:t1, j0:j1] = st.mean
+            se[f][t0:t1, j0:j1] = st.stderr
+            acc[f][0] += st.total_steps
+            acc[f][1] += st.kernel_ms
+            acc[f][2] += local
 
-    def field(f):
-        s = solvers[f]
+    def field(f, w):
+        s = solvers[2 * w + f]
         for g, (j0, j1, t0, t1) in enumerate(batches):
+            if g % k != w:
+                continue
             _, st = s.solve_sources(sc.points[j0:j1], srcs[t0:t1], nWalks=n_walks, maxSteps=sc.max_steps,
                                     eps=sc.eps, seed=group_seed(seed, g), return_stats=True)
             record(f, g, st, st.total_steps)
@@ -548,12 +566,13 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
     elif concurrent:
         from concurrent.futures import ThreadPoolExecutor
 
-        with ThreadPoolExecutor(max_workers=2) as ex:
-            for fut in [ex.submit(field, f) for f in range(2)]:
+        with ThreadPoolExecutor(max_workers=2 * k) as ex:
+            for fut in [ex.submit(field, f, w) for w in range(k) for f in range(2)]:
                 fut.result()
     else:
-        for f in range(2):
-            field(f)
+        for w in range(k):
+            for f in range(2):
+                field(f, w)
     steps, kms, launches = acc[0][0] + acc[1][0], acc[0][1] + acc[1][1], len(batches)
     q = np.arange(Q)
     M, N = quad[:, 1], quad[:, 2]

@@ -107,19 +107,29 @@ def _seed_of_group(g, seed=5):
     return survey.group_seed(seed, g)
 
 
-@pytest.mark.parametrize("R,walks", [(2, 3 * B + 100), (3, 5 * B), (2, B // 2)])
-def test_distributed_survey_equals_one_rank_with_one_collective_order(R, walks):
+@pytest.mark.parametrize("R,walks,pairs", [(2, 3 * B + 100, 1), (3, 5 * B, 1), (2, B // 2, 1), (2, 3 * B + 100, 2),
+                                           (3, 5 * B, 3)])
+def test_distributed_survey_equals_one_rank_with_one_collective_order(R, walks, pairs):
+    """... with `pairs` (model, background) handle pairs per rank: 2 x pairs worker
+    threads solve concurrently, the collective order stays the same."""
     from dcrmontecarlo_amd import survey
 
     sc = _scenario()
     one = survey.run_wenner_survey(sc, 1e-2, walks, seed=5, solvers=(FakeSolver(0.0), FakeSolver(0.5)))
+    many = survey.run_wenner_survey(sc, 1e-2, walks, seed=5,
+                                    solvers=sum(((FakeSolver(0.0, 0.005, seed=p), FakeSolver(0.5, 0.005, seed=7 + p))
+                                                 for p in range(pairs)), ()))
+    np.testing.assert_array_equal(many.model.dv, one.model.dv)
+    np.testing.assert_array_equal(many.background.se, one.background.se)
+    assert many.walk_steps == one.walk_steps
     rt = RankThreads(R)
     comms = {}
 
     def body(r, ar, ag):
         c = comms[r] = LoggedComm(r, R, ar, ag)
-        return survey.run_wenner_survey(sc, 1e-2, walks, seed=5, comm=c,
-                                        solvers=(FakeSolver(0.0, 0.01, seed=r), FakeSolver(0.5, 0.01, seed=9 + r)))
+        sv = sum(((FakeSolver(0.0, 0.01, seed=10 * r + p), FakeSolver(0.5, 0.01, seed=9 + 10 * r + p))
+                  for p in range(pairs)), ())
+        return survey.run_wenner_survey(sc, 1e-2, walks, seed=5, comm=c, solvers=sv)
 
     res = rt.run(body)
     for r in range(R):
@@ -161,9 +171,11 @@ def test_distributed_survey_failure_on_one_rank_reaches_every_rank():
     assert isinstance(res[0], Exception) and "another rank failed" in str(res[0])
 
 
-def test_survey_refuses_a_communicator_pair():
+def test_survey_refuses_a_communicator_pair_and_odd_handles():
     from dcrmontecarlo_amd import survey
 
     with pytest.raises(ValueError, match="one communicator"):
         survey.run_wenner_survey(_scenario(), 1e-2, 16, comm=(object(), object()),
                                  solvers=(FakeSolver(0.0), FakeSolver(0.5)))
+    with pytest.raises(ValueError, match="pairs"):
+        survey.run_wenner_survey(_scenario(), 1e-2, 16, solvers=(FakeSolver(0.0), FakeSolver(0.5), FakeSolver(1.0)))
