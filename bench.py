@@ -64,8 +64,9 @@ def parse():
                          "C5; the timed survey) or without it (physical); the rho_a report always comes from "
                          "a physical survey")
     ap.add_argument("--no-bruteforce", action="store_true", help="wenner_topography: skip the scan-kernel leg")
-    ap.add_argument("--handle-pairs", type=int, default=1,
-                    help="wenner_topography: (model, background) solver pairs, one host thread and HIP stream each")
+    ap.add_argument("--handle-pairs", type=int, default=3,
+                    help="wenner_topography: (model, background) solver pairs, one host thread and HIP stream each "
+                         "(1 / 2 / 3 pairs: 1.357 / 1.377 / 1.409e10 walk-steps/s, profiles/r04_ab/c5_handle_pairs_ab.log)")
     ap.add_argument("--electrodes", type=int, default=None,
                     help="dcr_dipole 48, wenner_topography 256, variable_coefficients 256 (query points)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")

@@ -526,11 +526,13 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "        return sPhi[seg];\n";
     }
     o << "    }\n};\n}  // namespace\n\n";
-    // waves per SIMD the register budget is sized for (tools/ab_bench.sh): 6, or 5 for the
-    // cooperative tree kernels, whose record visits load four children's words at once
-    // (profiles/r03_tree/tree_batch_waves_ab.log)
-    // (4 when the tree's records are staged: two 8-wave workgroups per CU)
-    int waves = tree ? (block != kWalkBlock ? 4 : 5) : 6;
+    // waves per SIMD the register budget is sized for: 7 for the scan kernels (their
+    // 256-thread workgroups are LDS-bound at 7 per CU either way; the 7-wave budget
+    // schedules C4 1.3% faster than 6: profiles/r04_ab/scan_waves_6_vs_7_ab.log), 5 for
+    // the cooperative tree kernels, whose record visits load four children's words at
+    // once (profiles/r03_tree/tree_batch_waves_ab.log), 4 when the tree's records are
+    // staged (one 16-wave or two 8-wave workgroups per CU)
+    int waves = tree ? (block != kWalkBlock ? 4 : 5) : 7;
     if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
     o << "extern \"C\" __global__ void __launch_bounds__(" << block << ", " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"
