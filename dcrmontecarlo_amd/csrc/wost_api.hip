@@ -227,6 +227,8 @@ struct wost_handle {
     int64_t points_cap = 0;
     float* d_point_alpha = nullptr;   // alpha at the query points (delta tracking)
     int64_t point_alpha_cap = 0;
+    uint32_t* d_pool = nullptr;       // walk pools of the tree kernels' workgroups (WalkArgs::pool)
+    int64_t pool_cap = 0;
     wost_timing timing{};
 };
 
@@ -518,7 +520,7 @@ void wost_destroy(wost_handle* h) {
     if (!h) return;
     if (h->device >= 0) (void)hipSetDevice(h->device);
     void* ptrs[] = {h->d_dverts, h->d_nverts, h->d_table, h->d_prog, h->d_counter, h->d_val,
-                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree, h->d_seg_phi, h->d_point_alpha};
+                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree, h->d_seg_phi, h->d_point_alpha, h->d_pool};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t& e : h->ev)
@@ -931,6 +933,31 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_lds_records = tree_lds;
         a.tree_lds_verts = tree_verts;
         a.tree_depth = h->tree.depth;
+        // walk pools (wost_walk.h): near = within WOST_POOL_NEAR (default 0.1) of the Neumann
+        // polyline's largest extent from its bounding box; WOST_TREE_POOL=0 turns them off,
+        // WOST_POOL_SLOTS (default 128) walks per class and workgroup
+        const char* pe = std::getenv("WOST_TREE_POOL");
+        if (!(pe && std::atoi(pe) == 0) && h->nverts.size() >= 4) {
+            float x0 = h->nverts[0], x1 = x0, y0 = h->nverts[1], y1 = y0;
+            for (size_t i = 2; i + 1 < h->nverts.size(); i += 2) {
+                x0 = std::min(x0, h->nverts[i]); x1 = std::max(x1, h->nverts[i]);
+                y0 = std::min(y0, h->nverts[i + 1]); y1 = std::max(y1, h->nverts[i + 1]);
+            }
+            float frac = 0.1f;
+            if (const char* e = std::getenv("WOST_POOL_NEAR")) frac = std::max(0.0f, (float)std::atof(e));
+            int slots = 128;
+            if (const char* e = std::getenv("WOST_POOL_SLOTS")) slots = std::max(1, std::min(4096, std::atoi(e)));
+            const float m = frac * std::max(x1 - x0, y1 - y0);
+            const int64_t words = (int64_t)pool_wg_words(ns, slots);
+            if ((rc = ensure_cap(h->d_pool, h->pool_cap, words * (int64_t)blocks_per_cu * h->num_cus)) != WOST_OK)
+                return rc;
+            a.pool = h->d_pool;
+            a.pool_slots = slots;
+            a.pool_wg_words = (int32_t)words;
+            a.pool_box = make_float4(x0 - m, y0 - m, x1 + m, y1 + m);
+            a.pool_near_waves = 2;   // WOST_POOL_NEAR_WAVES (0: by majority)
+            if (const char* e = std::getenv("WOST_POOL_NEAR_WAVES")) a.pool_near_waves = std::max(0, std::atoi(e));
+        }
     }
 
     if (mode_delta(mode) && n_points > 0) {   // alpha at the query points, with the walk kernel's fields

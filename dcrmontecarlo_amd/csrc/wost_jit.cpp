@@ -410,6 +410,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_TREE_SHARE " << std::max(0, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_DESCENT"))   // A/B: hand-outs during the descent
         o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
+    if (const char* e = std::getenv("WOST_JIT_POOL_MIN_PUSH"))   // A/B: fewest walks a wave parks
+        o << "#define WOST_POOL_MIN_PUSH " << std::max(1, std::min(64, std::atoi(e))) << "\n";
     if (tree && tree_stage >= 1) o << "#define WOST_TREE_STAGED 1\n";    // every record in LDS
     if (tree && tree_stage >= 2) o << "#define WOST_TREE_VSTAGED 1\n";   // and the Neumann vertices
     if (const char* e = std::getenv("WOST_JIT_TREE_QMARGIN"))   // A/B: per-query rounding scales

@@ -71,7 +71,23 @@ struct WalkArgs {
     int64_t base_pid;
     uint32_t base_off;
     int32_t small32;
+    // walk pools (TREE kernels, WOST_TREE_POOL; null: none): pool_wg_words words per
+    // workgroup, a 4-word header (lock, walks parked near, walks parked far) and then
+    // per class pool_slots parked walks of pool_fields(NS) words each (field-major);
+    // a walk is "near" while its point lies in pool_box (x0, y0, x1, y1)
+    uint32_t* pool;
+    int32_t pool_slots;
+    int32_t pool_wg_words;
+    float4 pool_box;
+    int32_t pool_near_waves;     // the workgroup's first pool_near_waves waves take the near walks
+                                 // (0: each wave takes the class most of its walks are in)
+    int32_t pool_pad;
 };
+
+// words of one parked walk: global id (2), local index (2), x, y, dD, step | onB << 31,
+// phi, w, alpha(x), then the NS source totals
+WOST_HD constexpr int pool_fields(int ns) { return 11 + ns; }
+WOST_HD constexpr int pool_wg_words(int ns, int slots) { return 4 + 2 * pool_fields(ns) * slots; }
 
 // alpha at the query points with the walk kernel's own Fields policy (the same
 // function the walk would evaluate at its start point, hence the same bits).
@@ -642,6 +658,42 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
 // GL: the polylines (and segment angles) are read from global memory instead of being
 // staged in LDS -- field-specialised kernels for polylines too long for the LDS budget
 // (wost_api.hip kGlobalPolylineLdsBytes).
+// Walk pools (TREE kernels): see the exchange in walk_body. WOST_TREE_POOL 0 compiles
+// them out; WOST_POOL_MIN_PUSH: fewest mismatched walks a wave parks at once.
+#ifndef WOST_TREE_POOL
+#define WOST_TREE_POOL 1
+#endif
+#ifndef WOST_POOL_MIN_PUSH
+#define WOST_POOL_MIN_PUSH 1
+#endif
+__device__ __forceinline__ bool pool_near(float4 b, float x, float y) {
+    return x >= b.x && x <= b.z && y >= b.y && y <= b.w;
+}
+// walks parked in class c (header word 1 + c), read with an atomic load so that every
+// read goes to memory (under the lock: exact; outside it: a hint)
+__device__ __forceinline__ uint32_t pool_count(uint32_t* pool, int c) {
+    return __hip_atomic_load(pool + 1 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// the pool lock (header word 0), taken by the wave's first lane for the whole wave; the
+// fences order the wave's slot reads and writes inside it
+__device__ __forceinline__ void pool_lock(uint32_t* pool, int lane) {
+    if (lane == 0) {
+        while (__hip_atomic_exchange(pool, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void pool_unlock(uint32_t* pool, int lane, uint32_t n_near, uint32_t n_far) {
+    if (lane == 0) {
+        __hip_atomic_store(pool + 1, n_near, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(pool + 2, n_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) __hip_atomic_store(pool, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 #ifndef WOST_REFILL_MIN   // idle lanes that trigger a refill (tools/ab_refill.sh; 1 = every iteration)
 #define WOST_REFILL_MIN 4
 #endif
@@ -715,6 +767,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         const float4* g = reinterpret_cast<const float4*>(A.table + kSamplerFloatsPadded);
         for (int i = threadIdx.x; i < kGnormCells; i += blockDim.x) sG[i] = g[i];
     }
+    // this workgroup's walk pools (header: lock, walks parked near, walks parked far)
+    uint32_t* const pool = (TREE && WOST_TREE_POOL && A.pool != nullptr)
+                               ? A.pool + (size_t)blockIdx.x * (size_t)A.pool_wg_words : nullptr;
+    if (pool != nullptr && threadIdx.x < 4) pool[threadIdx.x] = 0u;
     __syncthreads();
 
     const float sigma_bar = fld.sigma_bar();
@@ -778,6 +834,68 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         // lanes wait, so finished lanes idle until WOST_REFILL_MIN of them (or all
         // the wave's live ones) can start together. Each walk's result depends only
         // on its id, so the batching changes no bits.
+        // --- walk pools (TREE kernels): a wave pays its slowest lane's tree queries, and the
+        // lanes whose walks are near the Neumann polyline are the slow ones (C5: ~5% of the
+        // positions within 30 units of the topography cost ~5x the others). A wave whose
+        // walks are mostly far parks its near walks in the workgroup's near pool, and one
+        // whose walks are mostly near parks its far ones; freed lanes take parked walks of
+        // the wave's own class first, then new walks from the queue. A walk's state moves
+        // with it whole and its result depends only on its id: the bits do not change.
+        if (pool != nullptr && batch) {
+            const uint64_t act = __ballot(active);
+            const uint64_t nm = __ballot(active && pool_near(A.pool_box, px, py));
+            const int nact = __popcll(act), nnear = __popcll(nm);
+            const uint32_t hn = pool_count(pool, 0), hf = pool_count(pool, 1);
+            const int role = A.pool_near_waves > 0 ? ((int)(threadIdx.x >> 6) < A.pool_near_waves ? 0 : 1)
+                             : nact > 0 ? (2 * nnear > nact ? 0 : 1) : (hn >= hf ? 0 : 1);
+            uint64_t mis = role == 0 ? (act & ~nm) : nm;
+            if (exhausted || __popcll(mis) < WOST_POOL_MIN_PUSH) mis = 0ull;
+            if (mis != 0ull || (act != ~0ull && (role == 0 ? hn : hf) > 0u)) {
+                pool_lock(pool, lane);
+                uint32_t cnt[2] = {pool_count(pool, 0), pool_count(pool, 1)};
+                const int cm = 1 - role;
+                const uint32_t npush = min((uint32_t)__popcll(mis), (uint32_t)A.pool_slots - cnt[cm]);
+                const uint32_t rk = (uint32_t)__popcll(mis & lanes_below);
+                if ((mis & lanebit) && rk < npush) {
+                    uint32_t* const r = pool + 4 + (size_t)cm * pool_fields(NS) * A.pool_slots + cnt[cm] + rk;
+                    const int P = A.pool_slots;
+                    r[0 * P] = (uint32_t)wid; r[1 * P] = (uint32_t)(wid >> 32);
+                    r[2 * P] = (uint32_t)lid; r[3 * P] = (uint32_t)(lid >> 32);
+                    r[4 * P] = __builtin_bit_cast(uint32_t, px); r[5 * P] = __builtin_bit_cast(uint32_t, py);
+                    r[6 * P] = __builtin_bit_cast(uint32_t, dD);
+                    r[7 * P] = (uint32_t)k | (onB ? 0x80000000u : 0u);
+                    r[8 * P] = __builtin_bit_cast(uint32_t, phi); r[9 * P] = __builtin_bit_cast(uint32_t, w);
+                    r[10 * P] = __builtin_bit_cast(uint32_t, ax);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) r[(11 + s) * P] = __builtin_bit_cast(uint32_t, total[s]);
+                    active = false;
+                }
+                cnt[cm] += npush;
+                const uint64_t fr = __ballot(!active);
+                const uint32_t npull = min((uint32_t)__popcll(fr), cnt[role]);
+                const uint32_t rf = (uint32_t)__popcll(fr & lanes_below);
+                if (!active && rf < npull) {
+                    const uint32_t* const r =
+                        pool + 4 + (size_t)role * pool_fields(NS) * A.pool_slots + (cnt[role] - npull) + rf;
+                    const int P = A.pool_slots;
+                    wid = (uint64_t)r[0 * P] | (uint64_t)r[1 * P] << 32;
+                    lid = (uint64_t)r[2 * P] | (uint64_t)r[3 * P] << 32;
+                    px = __builtin_bit_cast(float, r[4 * P]); py = __builtin_bit_cast(float, r[5 * P]);
+                    dD = __builtin_bit_cast(float, r[6 * P]);
+                    const uint32_t kb = r[7 * P];
+                    k = (int)(kb & 0x7fffffffu); onB = (kb >> 31) != 0u;
+                    phi = __builtin_bit_cast(float, r[8 * P]); w = __builtin_bit_cast(float, r[9 * P]);
+                    ax = __builtin_bit_cast(float, r[10 * P]);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) total[s] = __builtin_bit_cast(float, r[(11 + s) * P]);
+                    pw = philox_walk(wid, A.key0, A.key1);
+                    if (WOST_PHILOX_AHEAD) rn_ahead = philox_draw(pw, (uint32_t)k, A.key0, A.key1);
+                    active = true;
+                }
+                cnt[role] -= npull;
+                pool_unlock(pool, lane, cnt[0], cnt[1]);
+            }
+        }
         uint64_t need = batch ? __ballot(!active) : 0ull;
         if (!kBatchEnd && __popcll(need) < WOST_REFILL_MIN && __any(active)) need = 0ull;
         while (need != 0ull && !exhausted) {
@@ -841,6 +959,40 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             }
             c_next += take;
             need = __ballot(!active);
+        }
+        // the queue is exhausted: idle lanes take parked walks of either class, and the
+        // wave ends only when both pools are empty (a wave parks walks only while the
+        // queue is not exhausted for it, and drains the pools itself before it ends)
+        if (pool != nullptr && exhausted && batch && __ballot(!active) != 0ull &&
+            (!__any(active) || pool_count(pool, 0) + pool_count(pool, 1) > 0u)) {
+            pool_lock(pool, lane);
+            uint32_t cnt[2] = {pool_count(pool, 0), pool_count(pool, 1)};
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const uint64_t fr = __ballot(!active);
+                const uint32_t npull = min((uint32_t)__popcll(fr), cnt[c]);
+                const uint32_t rf = (uint32_t)__popcll(fr & lanes_below);
+                if (!active && rf < npull) {
+                    const uint32_t* const r =
+                        pool + 4 + (size_t)c * pool_fields(NS) * A.pool_slots + (cnt[c] - npull) + rf;
+                    const int P = A.pool_slots;
+                    wid = (uint64_t)r[0 * P] | (uint64_t)r[1 * P] << 32;
+                    lid = (uint64_t)r[2 * P] | (uint64_t)r[3 * P] << 32;
+                    px = __builtin_bit_cast(float, r[4 * P]); py = __builtin_bit_cast(float, r[5 * P]);
+                    dD = __builtin_bit_cast(float, r[6 * P]);
+                    const uint32_t kb = r[7 * P];
+                    k = (int)(kb & 0x7fffffffu); onB = (kb >> 31) != 0u;
+                    phi = __builtin_bit_cast(float, r[8 * P]); w = __builtin_bit_cast(float, r[9 * P]);
+                    ax = __builtin_bit_cast(float, r[10 * P]);
+#pragma unroll
+                    for (int s = 0; s < NS; ++s) total[s] = __builtin_bit_cast(float, r[(11 + s) * P]);
+                    pw = philox_walk(wid, A.key0, A.key1);
+                    if (WOST_PHILOX_AHEAD) rn_ahead = philox_draw(pw, (uint32_t)k, A.key0, A.key1);
+                    active = true;
+                }
+                cnt[c] -= npull;
+            }
+            pool_unlock(pool, lane, cnt[0], cnt[1]);
         }
         if (!__any(active)) break;
         // a freshly refilled walk may already fail the while-condition (eps >= 1,

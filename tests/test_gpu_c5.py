@@ -146,3 +146,27 @@ def test_long_tree_with_wide_leaves_steps_down_its_staging(gpu_available):
     assert s.last_timing["tree"] == 0
     np.testing.assert_array_equal(ts, bs)
     np.testing.assert_array_equal(tv.view(np.uint32), bv.view(np.uint32))
+
+
+@pytest.mark.parametrize("env", [{"WOST_POOL_SLOTS": "1", "WOST_POOL_NEAR_WAVES": "0"},
+                                 {"WOST_POOL_SLOTS": "3", "WOST_POOL_NEAR_WAVES": "16", "WOST_POOL_NEAR": "1"},
+                                 {"WOST_POOL_NEAR_WAVES": "1", "WOST_POOL_NEAR": "0.01"}, {}])
+@pytest.mark.parametrize("physical", [False, True])
+def test_c5_walk_pools_change_no_bits(gpu_available, monkeypatch, env, physical):
+    """The tree kernels' walk pools (wost_walk.h) move whole walks between a workgroup's
+    waves: every walk's value and step count equal those without pools, for tiny pools
+    (one slot: constant parking pressure), near classes that take every walk, narrow
+    near margins, and the defaults."""
+    sc = _c5(physical=physical)
+    pts = sc.points[::4][:64]
+    monkeypatch.setenv("WOST_TREE_POOL", "0")
+    s0 = sc.solver(device=0)
+    v0, k0 = s0.solve_walks(pts, nWalks=1024, maxSteps=sc.max_steps, eps=sc.eps, seed=31)
+    assert s0.last_timing["tree"] == 1
+    monkeypatch.setenv("WOST_TREE_POOL", "1")
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    s1 = sc.solver(device=0)
+    v1, k1 = s1.solve_walks(pts, nWalks=1024, maxSteps=sc.max_steps, eps=sc.eps, seed=31)
+    np.testing.assert_array_equal(np.asarray(k1), np.asarray(k0))
+    np.testing.assert_array_equal(np.asarray(v1).view(np.uint32), np.asarray(v0).view(np.uint32))

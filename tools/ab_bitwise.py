@@ -15,7 +15,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIZES = {"laplace_square": (16, 4096), "manufactured_polynomial": (16, 4096), "poisson_square": (16, 4096),
          "variable_coefficients": (16, 4096), "dcr_dipole": (48, 16384), "notebook_dcr": (21, 4096),
-         "wenner_topography": (32, 512)}
+         "wenner_topography": (64, 2048), "wenner_topography_physical": (64, 2048)}
 
 
 def run_one(out):
@@ -26,7 +26,7 @@ def run_one(out):
     for name, (n, W) in SIZES.items():
         sc = S.ALL[name]()
         s = sc.solver(device=0)
-        pts = sc.points[:n] if name != "wenner_topography" else sc.points[::8][:n]
+        pts = sc.points[:n] if not name.startswith("wenner_topography") else sc.points[::4][:n]
         v, st = s.solve_walks(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=777)
         res[name + "_v"] = v
         res[name + "_s"] = st
