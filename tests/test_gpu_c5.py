@@ -170,3 +170,23 @@ def test_c5_walk_pools_change_no_bits(gpu_available, monkeypatch, env, physical)
     v1, k1 = s1.solve_walks(pts, nWalks=1024, maxSteps=sc.max_steps, eps=sc.eps, seed=31)
     np.testing.assert_array_equal(np.asarray(k1), np.asarray(k0))
     np.testing.assert_array_equal(np.asarray(v1).view(np.uint32), np.asarray(v0).view(np.uint32))
+
+
+def test_c5_walk_pools_change_no_bits_with_many_sources(gpu_available, monkeypatch):
+    """Multi-source walks (NS = 6: six totals travel with each parked walk) with one-slot
+    pools equal the solve without pools, value for value and step for step."""
+    from dcrmontecarlo_amd import survey
+
+    sc = _c5(n_electrodes=64, n_walks=512)
+    srcs = [survey.dipole_source(sc.points[q], sc.points[q + 3], 0.5) for q in range(0, 60, 10)]
+    pts = sc.points[::2][:32]
+    out = []
+    for env in ({"WOST_TREE_POOL": "0"}, {"WOST_TREE_POOL": "1", "WOST_POOL_SLOTS": "1", "WOST_POOL_NEAR_WAVES": "0"}):
+        for key, val in env.items():
+            monkeypatch.setenv(key, val)
+        s = sc.solver(device=0)
+        out.append(s.solve_sources_walks(pts, srcs, nWalks=512, maxSteps=sc.max_steps, eps=sc.eps, seed=9))
+    (v0, k0), (v1, k1) = out
+    assert v0.shape == (len(srcs), len(pts), 512)
+    np.testing.assert_array_equal(k1, k0)
+    np.testing.assert_array_equal(v1.view(np.uint32), v0.view(np.uint32))
