@@ -13,6 +13,23 @@ from ctypes import POINTER, c_double, c_float, c_int32, c_int64, c_uint8, c_uint
 
 import numpy as np
 
+
+def usable_cores() -> int:
+    """OMP_NUM_THREADS when set, else the CPUs this process may run on, capped by a cgroup
+    CPU quota (a GPU box shows the whole machine's CPUs but grants a share of them)."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = max(1, min(n, int(round(float(q) / float(per)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
@@ -126,7 +143,13 @@ class Problem:
         return np.array([lib.orc_sigma_prime(ctypes.byref(self.p), float(x), float(y)) for x, y in pts], np.float32)
 
     def solve_walks(self, points, n_walks, max_steps, eps, seed, wid_begin=0, wid_end=None, threads=0):
-        """Per-walk (values f32, steps u32) for global walks [wid_begin, wid_end)."""
+        """Per-walk (values f32, steps u32) for global walks [wid_begin, wid_end).
+        threads <= 0: every core this process may use (passed explicitly: OpenMP keeps the
+        last omp_set_num_threads of the process, so an earlier threads=1 call would
+        otherwise make every later default call single-threaded). The walks are
+        counter-based per walk id, so the thread count changes no result."""
+        if threads <= 0:
+            threads = usable_cores()
         pts = np.ascontiguousarray(points, np.float32).reshape(-1, 2)
         if wid_end is None:
             wid_end = pts.shape[0] * int(n_walks)
