@@ -412,11 +412,6 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
     if (const char* e = std::getenv("WOST_JIT_POOL_MIN_PUSH"))   // A/B: fewest walks a wave parks
         o << "#define WOST_POOL_MIN_PUSH " << std::max(1, std::min(64, std::atoi(e))) << "\n";
-    // A/B only: WOST_JIT_X2=1 runs two walks per lane in the scan kernels (walk_body_x2)
-    const char* x2e = std::getenv("WOST_JIT_X2");
-    const bool x2 = x2e && std::atoi(x2e) == 1 && !tree && !record && n_sources == 1 && !mode_fix(mode) &&
-                    !global_polylines;
-    if (x2) o << "#define WOST_WALK_X2 1\n";
     if (tree && tree_stage >= 1) o << "#define WOST_TREE_STAGED 1\n";    // every record in LDS
     if (tree && tree_stage >= 2) o << "#define WOST_TREE_VSTAGED 1\n";   // and the Neumann vertices
     if (const char* e = std::getenv("WOST_JIT_TREE_QMARGIN"))   // A/B: per-query rounding scales
@@ -545,15 +540,11 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
       << "wost_walk_jit(const wost::WalkArgs A) {\n"
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
       << "    const GenFields fld{reinterpret_cast<const float*>(A.prog + "
-      << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n";
-    if (x2)
-        o << "    wost::walk_body_x2<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
-          << (delta ? "true" : "false") << ">(A, fld, smem);\n}\n";
-    else
-        o << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
-          << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
-          << ", " << n_sources << ", " << (mode_fix(mode) ? "true" : "false") << ", "
-          << (global_polylines ? "true" : "false") << ">(A, fld, smem);\n}\n";
+      << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
+      << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
+      << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
+      << ", " << n_sources << ", " << (mode_fix(mode) ? "true" : "false") << ", "
+      << (global_polylines ? "true" : "false") << ">(A, fld, smem);\n}\n";
     if (delta)   // alpha at the query points, with these fields (WalkArgs::point_alpha)
         o << "extern \"C\" __global__ void __launch_bounds__(256)\n"
           << "wost_point_alpha_jit(const char* prog, const float2* pts, long long n, float* out) {\n"

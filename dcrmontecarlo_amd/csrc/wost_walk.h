@@ -1218,264 +1218,4 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     }
 }
 
-#if defined(WOST_WALK_X2)
-// A/B experiment (WOST_JIT_X2=1): two walks per lane, their step bodies
-// interleaved phase by phase so that each wave issues two independent instruction
-// streams (ILP instead of more waves). Field-specialised scan kernels only: no tree, no
-// recorder, one source, reference estimator, staged polylines. Every walk runs walk_body's
-// arithmetic in walk_body's order (its result depends only on its id): the same bits.
-template <bool NEU, bool SRC, bool DELTA, class F>
-__device__ __forceinline__ void walk_body_x2(const WalkArgs& A, const F& fld, unsigned char* smem) {
-#pragma clang fp contract(off)
-    constexpr bool kStageD = !F::kConstDirichlet;
-    constexpr bool kStageN = NEU;
-    unsigned char* lds = smem;
-    float4* sG = reinterpret_cast<float4*>(lds);
-    float* sT = reinterpret_cast<float*>(lds + (DELTA ? sizeof(float4) * (size_t)kGnormCells : 16));
-    lds += SRC ? align16((DELTA ? sizeof(float4) * (size_t)kGnormCells : 16) + sizeof(float) * kSamplerTailFloats) : 0;
-    float2* sD = reinterpret_cast<float2*>(lds);
-    lds += kStageD ? align16(sizeof(float2) * (size_t)A.nd) : 0;
-    float2* sN = reinterpret_cast<float2*>(lds);
-    lds += kStageN ? align16(sizeof(float2) * (size_t)A.nn) : 0;
-    float* sPhi = reinterpret_cast<float*>(lds);
-    if (kStageD)
-        for (int i = threadIdx.x; i < A.nd; i += blockDim.x) sD[i] = A.dverts[i];
-    if (kStageN) {
-        for (int i = threadIdx.x; i < A.nn; i += blockDim.x) sN[i] = A.nverts[i];
-        for (int i = threadIdx.x; i < A.nn - 1; i += blockDim.x) sPhi[i] = A.seg_phi[i];
-    }
-    float node0 = 0.0f;
-    if (SRC) {
-        node0 = A.table[0];
-        for (int i = threadIdx.x; i < kSamplerTailFloats; i += blockDim.x) sT[i] = A.table[i + 1];
-    }
-    if (DELTA) {
-        const float4* g = reinterpret_cast<const float4*>(A.table + kSamplerFloatsPadded);
-        for (int i = threadIdx.x; i < kGnormCells; i += blockDim.x) sG[i] = g[i];
-    }
-    __syncthreads();
-    const float sigma_bar = fld.sigma_bar();
-    const float inv_sb = fld.inv_sigma_bar();
-    const float sqrt_sb = fld.sqrt_sigma_bar();
-    const int lane = threadIdx.x & 63;
-    const uint64_t lanebit = 1ull << lane;
-    const uint64_t lanes_below = lanebit - 1ull;
-    uint64_t c_next = 0, c_end = 0;
-    bool exhausted = false;
-    bool active[2] = {false, false};
-    PhiloxWalk pw[2] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-    uint64_t lid[2] = {0, 0};
-    float px[2] = {0.f, 0.f}, py[2] = {0.f, 0.f}, dD[2] = {1.f, 1.f}, phi[2] = {0.f, 0.f};
-    float w[2] = {1.f, 1.f}, ax[2] = {1.f, 1.f}, total[2] = {0.f, 0.f};
-    int k[2] = {0, 0};
-    bool onB[2] = {false, false};
-    for (;;) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {   // termination (:206, :295-298)
-            if (active[j] && !((k[j] < A.max_steps) && (dD[j] > A.eps))) {
-                float g = fld.has_g() ? fld.g(px[j], py[j]) : 0.0f;
-                if (DELTA) g = g * w[j];
-                total[j] = total[j] + g;
-                A.out_val[(int64_t)lid[j]] = total[j];
-                A.out_steps[(int64_t)lid[j]] = (uint32_t)k[j];
-                active[j] = false;
-            }
-        }
-        // refill: the wave's 128 walk slots, slot 0 of every lane first
-        uint64_t need0 = __ballot(!active[0]), need1 = __ballot(!active[1]);
-        if (__popcll(need0) + __popcll(need1) < WOST_REFILL_MIN && __any(active[0] || active[1])) need0 = need1 = 0ull;
-        while ((need0 | need1) != 0ull && !exhausted) {
-            if (c_next >= c_end) {
-                unsigned long long c = 0;
-                if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)A.chunk);
-                c = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(c >> 32)) << 32) |
-                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c);
-                if (c >= (unsigned long long)A.count) {
-                    exhausted = true;
-                    break;
-                }
-                c_next = c;
-                c_end = c + (uint64_t)A.chunk;
-                if (c_end > (uint64_t)A.count) c_end = (uint64_t)A.count;
-            }
-            const uint64_t avail = c_end - c_next;
-            const uint32_t n0 = (uint32_t)__popcll(need0);
-            const uint32_t n = n0 + (uint32_t)__popcll(need1);
-            const uint32_t take = avail < (uint64_t)n ? (uint32_t)avail : n;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const uint64_t nj = j == 0 ? need0 : need1;
-                const uint32_t rank = (j == 0 ? 0u : n0) + (uint32_t)__popcll(nj & lanes_below);
-                if ((nj & lanebit) && rank < take) {
-                    lid[j] = c_next + rank;
-                    uint64_t pid, wid;
-                    if (A.range_walks > 0) {
-                        const uint32_t l32 = (uint32_t)lid[j], rw = (uint32_t)A.range_walks;
-                        uint32_t q = (uint32_t)((double)l32 * A.inv_range_walks);
-                        int32_t rem = (int32_t)(l32 - q * rw);
-                        if (rem < 0) { --q; rem += (int32_t)rw; }
-                        else if (rem >= (int32_t)rw) { ++q; rem -= (int32_t)rw; }
-                        pid = (uint64_t)A.range_point0 + q;
-                        wid = pid * (uint64_t)A.walks_per_point + (uint64_t)A.range_offset + (uint64_t)rem;
-                    } else if (A.small32) {
-                        const uint32_t local = A.base_off + (uint32_t)lid[j], w32 = (uint32_t)A.walks_per_point;
-                        uint32_t q = (uint32_t)((double)local * A.inv_walks_per_point);
-                        const int32_t rem = (int32_t)(local - q * w32);
-                        if (rem < 0) --q;
-                        else if (rem >= (int32_t)w32) ++q;
-                        pid = (uint64_t)A.base_pid + q;
-                        wid = (uint64_t)A.wid_begin + lid[j];
-                    } else {
-                        wid = (uint64_t)A.wid_begin + lid[j];
-                        pid = (uint64_t)((double)wid * A.inv_walks_per_point);
-                        const int64_t rem = (int64_t)(wid - pid * (uint64_t)A.walks_per_point);
-                        if (rem < 0) --pid;
-                        else if (rem >= A.walks_per_point) ++pid;
-                    }
-                    pw[j] = philox_walk(wid, A.key0, A.key1);
-                    const float2 q = A.points[pid];
-                    px[j] = q.x; py[j] = q.y;
-                    k[j] = 0; dD[j] = 1.0f; onB[j] = false; phi[j] = 0.f; w[j] = 1.f; total[j] = 0.f;
-                    if (DELTA) ax[j] = A.point_alpha[pid];
-                    active[j] = true;
-                }
-            }
-            c_next += take;
-            need0 = __ballot(!active[0]);
-            need1 = __ballot(!active[1]);
-        }
-        if (!__any(active[0] || active[1])) break;
-        bool stepping[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) stepping[j] = active[j] && (k[j] < A.max_steps) && (dD[j] > A.eps);
-        if (!__any(stepping[0] || stepping[1])) continue;
-
-        // --- both walks' steps (:206-291), phase by phase
-        float dd[2], r[2], cs[2], sn[2], xnx[2], xny[2], nphi[2];
-        bool nonB[2];
-        U4 rn[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) dd[j] = fld.dirichlet_distance(sD, A.nd, px[j], py[j]);   // :208
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            if (NEU) {
-                const float dn = fld.neumann_silhouette_distance(sN, A.nn, px[j], py[j]);    // :211
-                const float m = dn < dd[j] ? dn : dd[j];
-                r[j] = m > A.rmin ? m : A.rmin;                                              // :212
-            } else {
-                r[j] = dd[j] > A.rmin ? dd[j] : A.rmin;                                      // :215
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {   // :226-232
-            uint32_t key0 = A.key0, key1 = A.key1;
-            WOST_OPAQUE_SGPR(key0);
-            WOST_OPAQUE_SGPR(key1);
-            rn[j] = philox_draw(pw[j], (uint32_t)k[j], key0, key1);
-            float theta = (u01(rn[j].x) * 2.0f) * kPiF;
-            if (NEU && onB[j]) theta = theta / 2.0f + phi[j];
-            cs[j] = f_cos(theta);
-            sn[j] = f_sin(theta);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {   // :235-239
-            if (NEU) {
-                const Hit h = fld.neumann_intersect(sN, A.nn, px[j], py[j], cs[j], sn[j], r[j]);
-                xnx[j] = h.x; xny[j] = h.y; nonB[j] = h.hit;
-                nphi[j] = h.hit ? fld.neumann_phi(sPhi, h.seg) : phi[j];
-            } else {
-                xnx[j] = px[j] + r[j] * cs[j];
-                xny[j] = py[j] + r[j] * sn[j];
-                nonB[j] = onB[j];
-                nphi[j] = phi[j];
-            }
-        }
-        float yx[2] = {xnx[0], xnx[1]}, yy[2] = {xny[0], xny[1]}, c[2] = {0.f, 0.f}, gnorm[2] = {0.f, 0.f};
-        bool clipped[2] = {false, false};
-        Jet aj[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-        if (SRC) {
-            float a2[2], b2[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {   // :244-248
-                const float rs = sample_rho_tail(sT, node0, u01(rn[j].y)) * r[j];
-                yx[j] = px[j] + rs * cs[j];
-                yy[j] = py[j] + rs * sn[j];
-                const float e1x = yx[j] - px[j], e1y = yy[j] - py[j];
-                const float e2x = xnx[j] - px[j], e2y = xny[j] - py[j];
-                a2[j] = e1x * e1x + e1y * e1y;
-                b2[j] = e2x * e2x + e2y * e2y;
-            }
-            if (WOST_ANY(a2[0] > b2[0] || a2[1] > b2[1])) {
-                WOST_NO_SPECULATION();
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    if (a2[j] > b2[j]) clipped[j] = sqrtf(a2[j]) > sqrtf(b2[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                if (clipped[j]) { yx[j] = xnx[j]; yy[j] = xny[j]; }
-            if (DELTA) {
-#pragma unroll
-                for (int j = 0; j < 2; ++j) gnorm[j] = greens_norm_from_table(sG, r[j] * sqrt_sb, r[j], inv_sb);
-#pragma unroll
-                for (int j = 0; j < 2; ++j) aj[j] = fld.alpha_jet(yx[j], yy[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {   // :249-258
-                if (!clipped[j]) {
-                    const float f = fld.f(yx[j], yy[j]);
-                    if (DELTA)
-                        c[j] = (f * gnorm[j]) * f_rsq(aj[j].v * ax[j]) * w[j];
-                    else
-                        c[j] = f * ((r[j] * r[j]) / 4.0f);
-                }
-            }
-        }
-        float npx[2], npy[2], nw[2], nax[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) { npx[j] = xnx[j]; npy[j] = xny[j]; nw[j] = w[j]; nax[j] = ax[j]; }
-        if (DELTA) {   // :271-284
-            bool accept[2];
-            float anew[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                accept[j] = u01(rn[j].z) > sigma_bar * gnorm[j];
-                anew[j] = aj[j].v;
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                if (accept[j] && !clipped[j]) anew[j] = fld.alpha(xnx[j], xny[j]);
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                float sc = 1.0f;
-                if (!accept[j]) {
-                    const float spv = sigma_prime_from(aj[j], fld.sigma(yx[j], yy[j]), fld.detached());
-                    sc = 1.0f - spv * inv_sb;
-                    sc = (0.0f > sc) ? 0.0f : sc;
-                }
-                const float wt = w[j] * f_sqrt(f_div(anew[j], ax[j]));
-                nw[j] = accept[j] ? wt : wt * sc;
-                npx[j] = accept[j] ? xnx[j] : yx[j];
-                npy[j] = accept[j] ? xny[j] : yy[j];
-                nax[j] = anew[j];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {   // the step's state, for the walks that took it
-            if (stepping[j]) {
-                if (SRC) total[j] = total[j] + c[j];
-                onB[j] = nonB[j];
-                phi[j] = nphi[j];
-                w[j] = nw[j];
-                ax[j] = nax[j];
-                px[j] = npx[j];
-                py[j] = npy[j];
-                k[j] += 1;
-                dD[j] = dd[j];
-            }
-        }
-    }
-}
-#endif
-
 }  // namespace wost

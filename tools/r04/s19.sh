@@ -3,6 +3,7 @@
 # against one -- bits, then the scan scenarios' rates at 5 and 6 waves per SIMD,
 # alternated, then the bench line both ways.
 set -o pipefail
+# (Not adopted: the two-walk kernel exists only in commit e65523c; profiles/r04_ab/two_walks_per_lane_ab.log.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r04s19
 mkdir -p $O
