@@ -190,3 +190,18 @@ def test_c5_walk_pools_change_no_bits_with_many_sources(gpu_available, monkeypat
     assert v0.shape == (len(srcs), len(pts), 512)
     np.testing.assert_array_equal(k1, k0)
     np.testing.assert_array_equal(v1.view(np.uint32), v0.view(np.uint32))
+
+
+def test_c5_walk_pools_change_no_bits_in_walk_range_solves(gpu_available, monkeypatch):
+    """Walk-range solves (wost_solve_range, the multi-GPU shard unit: a launch's local
+    walks map to point ranges) with one-slot pools equal those without pools."""
+    sc = _c5()
+    pts = sc.points[::8][:24]
+    out = []
+    for env in ({"WOST_TREE_POOL": "0"}, {"WOST_TREE_POOL": "1", "WOST_POOL_SLOTS": "1", "WOST_POOL_NEAR_WAVES": "1"}):
+        for key, val in env.items():
+            monkeypatch.setenv(key, val)
+        s = sc.solver(device=0)
+        out.append(s.solve_range(pts, 8192, 4096, 8192, sc.max_steps, sc.eps, 21))
+    assert out[0].shape[0] == len(pts)
+    np.testing.assert_array_equal(out[1], out[0])
