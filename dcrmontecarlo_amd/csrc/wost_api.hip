@@ -241,6 +241,13 @@ constexpr int64_t kMaxBatchWalks = int64_t(1) << 26;   // 64 Mi walks = 512 MiB 
 // polylines under compat="fixed" (which scans them), work at any length.
 constexpr size_t kGlobalPolylineLdsBytes = 40 * 1024;
 
+// study builds: WOST_TREE_ITER_STATS=1 compiles the tree queries' loop counters into the
+// field-specialised kernels (wost_walk.h) and prints their sums after each solve
+bool tree_iter_stats() {
+    const char* e = std::getenv("WOST_TREE_ITER_STATS");
+    return e && std::atoi(e) == 1;
+}
+
 int upload_program(wost_handle* h) {
     if (!h->prog_dirty) return WOST_OK;
     build_program(h->fields, h->sigma_bar, h->prog);
@@ -948,13 +955,17 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
             int slots = 128;
             if (const char* e = std::getenv("WOST_POOL_SLOTS")) slots = std::max(1, std::min(4096, std::atoi(e)));
             const float m = frac * std::max(x1 - x0, y1 - y0);
-            const int64_t words = (int64_t)pool_wg_words(ns, slots);
+            // (study builds, WOST_TREE_ITER_STATS=1: 16 counter words after each workgroup's pools)
+            const int64_t words = (int64_t)pool_wg_words(ns, slots) + (tree_iter_stats() ? 16 : 0);
             if ((rc = ensure_cap(h->d_pool, h->pool_cap, words * (int64_t)blocks_per_cu * h->num_cus)) != WOST_OK)
                 return rc;
             a.pool = h->d_pool;
             a.pool_slots = slots;
             a.pool_wg_words = (int32_t)words;
             a.pool_box = make_float4(x0 - m, y0 - m, x1 + m, y1 + m);
+            if (tree_iter_stats())
+                HIP_TRY(hipMemsetAsync(h->d_pool, 0, sizeof(uint32_t) * (size_t)(words * blocks_per_cu * h->num_cus),
+                                       h->stream));
             a.pool_near_waves = 2;   // WOST_POOL_NEAR_WAVES (0: by majority)
             if (const char* e = std::getenv("WOST_POOL_NEAR_WAVES")) a.pool_near_waves = std::max(0, std::atoi(e));
         }
@@ -1062,6 +1073,18 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         ++launches;
         walks_done += count;
         j = j2;
+    }
+    if (tree_iter_stats() && a.pool != nullptr) {   // study builds: the tree queries' loop counters
+        const int64_t nwg = (int64_t)blocks_per_cu * h->num_cus;
+        std::vector<uint32_t> pw((size_t)(a.pool_wg_words * nwg));
+        HIP_TRY(hipMemcpy(pw.data(), a.pool, sizeof(uint32_t) * pw.size(), hipMemcpyDeviceToHost));
+        const int64_t off = a.pool_wg_words - 16;
+        double c[16] = {};
+        for (int64_t g = 0; g < nwg; ++g)
+            for (int i = 0; i < 16; ++i) c[i] += pw[(size_t)(g * a.pool_wg_words + off + i)];
+        std::fprintf(stderr, "tree_iter_stats:");
+        for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %.0f", c[i]);
+        std::fprintf(stderr, "\n");
     }
     std::vector<double> bs(row * nblk);
     HIP_TRY(hipMemcpyAsync(bs.data(), h->d_bstats, sizeof(double) * row * nblk, hipMemcpyDeviceToHost, h->stream));

@@ -184,6 +184,20 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 #ifndef WOST_TREE_SHARE_MIN   // ... and at least this many subtrees are pending
 #define WOST_TREE_SHARE_MIN 1
 #endif
+#ifndef WOST_TREE_QUAD   // the ray query's visits tested by quads of lanes (one child per lane)
+#define WOST_TREE_QUAD 0
+#endif
+// the n lowest set bits of m (wave-uniform: scalar work)
+__device__ __forceinline__ uint64_t lowest_set_bits(uint64_t m, int n) {
+    if (__popcll(m) <= n) return m;
+    int lo = 0, hi = 64;   // the smallest k with popcount(m & (2^k - 1)) >= n lies in (lo, hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (__popcll(m & ((1ull << mid) - 1ull)) >= n) hi = mid;
+        else lo = mid;
+    }
+    return m & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull));
+}
 #ifndef WOST_TREE_BATCH   // children of a record whose words are loaded together (1, 2 or 4)
 #define WOST_TREE_BATCH 4
 #endif
@@ -250,9 +264,10 @@ __device__ __forceinline__ bool tree_hand_out(TreeWaveScratch* ws, uint64_t live
 
 // silhouette_distance_tree (wost_device.h), the wave's lanes sharing the search;
 // `want`: this lane has a query. Same use contract (exact below dd and above rmin).
+// (ic: loop counters of a WOST_TREE_ITER_STATS study build, else null and compiled away)
 __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t, float px, float py, float dd,
                                                                float stop2, bool want, TreeWaveScratch* ws,
-                                                               int lane) {
+                                                               int lane, uint32_t* ic = nullptr) {
 #pragma clang fp contract(off)
     const uint64_t lanes_below = (1ull << lane) - 1ull;
     const int nv = t.nv, nseg = nv - 1;
@@ -280,6 +295,10 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
         plb3 = l == 3 ? x : plb3; plb4 = l == 4 ? x : plb4;
     };
     auto visit = [&](int lvl, int at, uint32_t cand, int& nj, float& nb2) {
+        if (ic) {
+            ic[3] += 1u;                                                     // lane-visits
+            if (lane == (int)__builtin_ctzll(__ballot(1))) ic[15] += 1u;    // the wave's visit issues
+        }
         const int k = tree_level_offset(lvl) + at;
         const float bound = best < T ? best : T;
         uint32_t kept = 0u;
@@ -338,6 +357,7 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
         const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
         const PendCount pc = wave_pend_count(n);
         if (WOST_TREE_SHARE_MIN > 1 && pc.total < WOST_TREE_SHARE_MIN) return;
+        if (ic) ic[4] += 1u;
         // every lane leaves what it found in its owner's slot, then takes the owner's
         // best so far as its bound
         if (best < WOST_INF) atomicMin(&ws->slot[owner], (unsigned long long)__builtin_bit_cast(uint32_t, best));
@@ -355,16 +375,19 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
         best = sb < best ? sb : best;
         if (live && best <= stop2) { live = false; pend = 0u; }
     };
+    if (ic) ic[0] += 1u;
     wave_lds_sync();
     for (;;) {
         const uint64_t L = __ballot(live);
         if (L == 0ull) break;
+        if (ic) ic[1] += 1u;
         share(L);
 #if WOST_TREE_SHARE_DESCENT
         // the descent as a uniform loop, so that a hand-out can run at every level
         for (;;) {
             const bool down = live && d < t.depth;
             if (!__any(down)) break;
+            if (ic) ic[2] += 1u;
             if (down) {
 #else
         {
@@ -387,7 +410,9 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
 #endif
         }
         // (no `continue` in this loop: every lane must reach the next ballot)
+        if (ic && __any(live)) ic[6] += 1u;
         if (live) {
+            if (ic) ic[5] += 1u;
             const int s0 = pos * t.leaf;
             const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
             const int j1 = s1 < nv - 2 ? s1 : nv - 2;
@@ -440,7 +465,7 @@ __device__ __forceinline__ float silhouette_distance_tree_wave(const SegTree& t,
 template <bool NORMAL = true, bool NEAREST = false>
 __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, float px, float py, float dxi,
                                                              float dyi, float r, bool want, TreeWaveScratch* ws,
-                                                             int lane) {
+                                                             int lane, uint32_t* ic = nullptr) {
 #pragma clang fp contract(off)
     const uint64_t lanes_below = (1ull << lane) - 1ull;
     float dn, dx, dy;
@@ -455,8 +480,8 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
     float best = WOST_INF;
     int bi = -1;
     bool live = want && !degenerate;
-    // the pruning of intersect_polylines_tree's keep()
-    auto keep = [&](float4 cu, float4 ab) {
+    // the pruning of intersect_polylines_tree's keep(), for the query (qx, qy, ddx, ddy, tol)
+    auto keep_q = [&](float4 cu, float4 ab, float qx, float qy, float ddx, float ddy, float tol) {
         if (ab.x < 0.0f) return false;
         const float cx = cu.x - qx, cy = cu.y - qy;
         const float cr = ddx * cu.w - ddy * cu.z, dt = ddx * cu.z + ddy * cu.w;
@@ -471,6 +496,7 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         return true;
 #endif
     };
+    auto keep = [&](float4 cu, float4 ab) { return keep_q(cu, ab, qx, qy, ddx, ddy, tol); };
     int d = 0, pos = 0;
     uint32_t pend = 0u;
     auto resume = [&]() {
@@ -494,6 +520,7 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         const uint32_t n = live ? (uint32_t)__popcll(pend) : 0u;
         const PendCount pc = wave_pend_count(n);
         if (WOST_TREE_SHARE_MIN > 1 && pc.total < WOST_TREE_SHARE_MIN) return;
+        if (ic) ic[11] += 1u;
         deposit();
         if (tree_hand_out(ws, L, live, n, pc, lanes_below, owner, d, pos, pend)) {
             live = true;
@@ -506,20 +533,67 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         ddy = __shfl(dy, owner);
         tol = __shfl(tol0, owner);
     };
+    if (ic) ic[7] += 1u;
     wave_lds_sync();
     for (;;) {
         const uint64_t L = __ballot(live);
         if (L == 0ull) break;
+        if (ic) ic[8] += 1u;
         share(L);
+#if WOST_TREE_QUAD
+        // the descent with each visit's four child tests spread over a quad of lanes: up to
+        // 16 descending lanes per batch, lane 4q + c tests child c of the q-th one's node
+        // for its query; one ballot returns every visit's kept mask (the same tests on the
+        // same values as the lane's own visit, so the same traversal)
+        for (;;) {
+            const uint64_t D = __ballot(live && d < t.depth);
+            if (D == 0ull) break;
+            if (ic) ic[9] += 1u;
+            uint64_t rem = D;
+            while (rem != 0ull) {
+                const uint64_t batch = lowest_set_bits(rem, 16);
+                rem &= ~batch;
+                const bool mine = (batch & (1ull << lane)) != 0ull;
+                const uint32_t rk = (uint32_t)__popcll(batch & lanes_below);
+                if (mine) ws->task[rk] = (uint32_t)lane;
+                wave_lds_sync();
+                const int q = lane >> 2, c = lane & 3;
+                const bool tester = q < __popcll(batch);
+                const int src = tester ? (int)ws->task[q] : lane;
+                wave_lds_sync();   // task[] is rewritten by the next batch and the hand-outs
+                const int sk = __shfl(tree_level_offset(d) + pos, src);
+                const float sqx = __shfl(qx, src), sqy = __shfl(qy, src);
+                const float sdx = __shfl(ddx, src), sdy = __shfl(ddy, src), stol = __shfl(tol, src);
+                bool kc = false;
+                if (tester) kc = keep_q(t.word(sk, 2 * c), t.word(sk, 2 * c + 1), sqx, sqy, sdx, sdy, stol);
+                const uint64_t kb = __ballot(kc);
+                if (mine) {
+                    if (ic) ic[10] += 1u;
+                    const uint32_t kept = (uint32_t)(kb >> (4 * rk)) & 15u;
+                    if (kept) {
+                        const int j = lowest_bit(kept);
+                        pend |= (kept & ~(1u << j)) << (4 * d);
+                        pos = 4 * pos + j;
+                        ++d;
+                    } else {
+                        live = resume();
+                    }
+                }
+            }
+            share(__ballot(live));
+        }
+#else
 #if WOST_TREE_SHARE_DESCENT
         for (;;) {
             const bool down = live && d < t.depth;
             if (!__any(down)) break;
+            if (ic) ic[9] += 1u;
             if (down) {
 #else
         {
             while (live && d < t.depth) {
 #endif
+                if (ic) ic[10] += 1u;
                 const int k = tree_level_offset(d) + pos;
                 uint32_t kept = 0u;
 #pragma unroll
@@ -544,8 +618,11 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
             share(__ballot(live));
 #endif
         }
+#endif
         const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
+        if (ic && __any(live && s0 < s1)) ic[13] += 1u;
+        if (ic && live && s0 < s1) ic[12] += 1u;
         if (NEAREST && live && s0 < s1) {
             float2 a = t.vert(s0);
             for (int i0 = s0; i0 < s1; i0 += 4) {   // vertices loaded four at a time
@@ -801,6 +878,14 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     float total[NS];            // this walk's contributions (one per source)
 #pragma unroll
     for (int s = 0; s < NS; ++s) total[s] = 0.f;
+#if defined(WOST_TREE_ITER_STATS)   // study build: the tree queries' loop counters (WOST_IC)
+    uint32_t ic_arr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ic_arr[i] = 0u;
+#define WOST_IC (TREE ? ic_arr : nullptr)
+#else
+#define WOST_IC nullptr
+#endif
 
     // Tree kernels (long walks) also defer a finished walk's end record and output
     // into the refill batch: it idles until WOST_REFILL_MIN lanes are finished or
@@ -1003,6 +1088,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         if (kWaveTree ? !__any(stepping) : !stepping) continue;
 
         // --- one walk-step (:206-291)
+#if defined(WOST_TREE_ITER_STATS)
+        ic_arr[14] += 1u;
+#endif
         const float dd = fld.dirichlet_distance(dP, A.nd, px, py);  // :208
         if (FIX && stepping && !(dd > A.eps)) {   // Q7/Q12 fixed: stop here, g at this point
             dD = dd;
@@ -1046,7 +1134,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #if defined(WOST_ABL_NO_SILHOUETTE)   // ablation (timing only)
             const float dn = WOST_INF;
 #else
-            const float dn = kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane)
+            const float dn = kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane,
+                                                                       WOST_IC)
                            : TREE      ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
                                        : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
 #endif
@@ -1072,7 +1161,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #if defined(WOST_ABL_NO_RAY)
             Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
 #else
-            const Hit h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws, lane)
+            const Hit h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws,
+                                                                                lane, WOST_IC)
                           : FIX       ? fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r)
                                       : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
 #endif
@@ -1216,6 +1306,16 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         k += 1;                                                      // :291
         dD = dd;   // the loop tests the distance of the pre-step point (quirk Q7)
     }
+#if defined(WOST_TREE_ITER_STATS)
+    // each lane's counters into the workgroup's study words after its pools (the host
+    // sizes A.pool for them when WOST_TREE_ITER_STATS is set)
+    if (pool != nullptr) {
+        uint32_t* const st = pool + 4 + 2 * (size_t)pool_fields(NS) * A.pool_slots;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) atomicAdd(st + i, ic_arr[i]);
+    }
+#endif
+#undef WOST_IC
 }
 
 }  // namespace wost
