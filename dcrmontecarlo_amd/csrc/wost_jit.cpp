@@ -414,8 +414,6 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "#define WOST_POOL_MIN_PUSH " << std::max(1, std::min(64, std::atoi(e))) << "\n";
     if (const char* e = std::getenv("WOST_TREE_ITER_STATS"))   // study build: loop counters
         if (std::atoi(e) == 1 && tree) o << "#define WOST_TREE_ITER_STATS 1\n";
-    if (const char* e = std::getenv("WOST_JIT_TREE_QUAD"))   // A/B: quad-cooperative ray visits
-        o << "#define WOST_TREE_QUAD " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
     if (tree && tree_stage >= 1) o << "#define WOST_TREE_STAGED 1\n";    // every record in LDS
     if (tree && tree_stage >= 2) o << "#define WOST_TREE_VSTAGED 1\n";   // and the Neumann vertices
     if (const char* e = std::getenv("WOST_JIT_TREE_QMARGIN"))   // A/B: per-query rounding scales

@@ -184,20 +184,6 @@ WOST_HD size_t walk_lds_bytes_for(bool neu, bool src, int nd, int nn, int n_poin
 #ifndef WOST_TREE_SHARE_MIN   // ... and at least this many subtrees are pending
 #define WOST_TREE_SHARE_MIN 1
 #endif
-#ifndef WOST_TREE_QUAD   // the ray query's visits tested by quads of lanes (one child per lane)
-#define WOST_TREE_QUAD 0
-#endif
-// the n lowest set bits of m (wave-uniform: scalar work)
-__device__ __forceinline__ uint64_t lowest_set_bits(uint64_t m, int n) {
-    if (__popcll(m) <= n) return m;
-    int lo = 0, hi = 64;   // the smallest k with popcount(m & (2^k - 1)) >= n lies in (lo, hi]
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (__popcll(m & ((1ull << mid) - 1ull)) >= n) hi = mid;
-        else lo = mid;
-    }
-    return m & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull));
-}
 #ifndef WOST_TREE_BATCH   // children of a record whose words are loaded together (1, 2 or 4)
 #define WOST_TREE_BATCH 4
 #endif
@@ -480,8 +466,8 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
     float best = WOST_INF;
     int bi = -1;
     bool live = want && !degenerate;
-    // the pruning of intersect_polylines_tree's keep(), for the query (qx, qy, ddx, ddy, tol)
-    auto keep_q = [&](float4 cu, float4 ab, float qx, float qy, float ddx, float ddy, float tol) {
+    // the pruning of intersect_polylines_tree's keep()
+    auto keep = [&](float4 cu, float4 ab) {
         if (ab.x < 0.0f) return false;
         const float cx = cu.x - qx, cy = cu.y - qy;
         const float cr = ddx * cu.w - ddy * cu.z, dt = ddx * cu.z + ddy * cu.w;
@@ -496,7 +482,6 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         return true;
 #endif
     };
-    auto keep = [&](float4 cu, float4 ab) { return keep_q(cu, ab, qx, qy, ddx, ddy, tol); };
     int d = 0, pos = 0;
     uint32_t pend = 0u;
     auto resume = [&]() {
@@ -540,49 +525,6 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
         if (L == 0ull) break;
         if (ic) ic[8] += 1u;
         share(L);
-#if WOST_TREE_QUAD
-        // the descent with each visit's four child tests spread over a quad of lanes: up to
-        // 16 descending lanes per batch, lane 4q + c tests child c of the q-th one's node
-        // for its query; one ballot returns every visit's kept mask (the same tests on the
-        // same values as the lane's own visit, so the same traversal)
-        for (;;) {
-            const uint64_t D = __ballot(live && d < t.depth);
-            if (D == 0ull) break;
-            if (ic) ic[9] += 1u;
-            uint64_t rem = D;
-            while (rem != 0ull) {
-                const uint64_t batch = lowest_set_bits(rem, 16);
-                rem &= ~batch;
-                const bool mine = (batch & (1ull << lane)) != 0ull;
-                const uint32_t rk = (uint32_t)__popcll(batch & lanes_below);
-                if (mine) ws->task[rk] = (uint32_t)lane;
-                wave_lds_sync();
-                const int q = lane >> 2, c = lane & 3;
-                const bool tester = q < __popcll(batch);
-                const int src = tester ? (int)ws->task[q] : lane;
-                wave_lds_sync();   // task[] is rewritten by the next batch and the hand-outs
-                const int sk = __shfl(tree_level_offset(d) + pos, src);
-                const float sqx = __shfl(qx, src), sqy = __shfl(qy, src);
-                const float sdx = __shfl(ddx, src), sdy = __shfl(ddy, src), stol = __shfl(tol, src);
-                bool kc = false;
-                if (tester) kc = keep_q(t.word(sk, 2 * c), t.word(sk, 2 * c + 1), sqx, sqy, sdx, sdy, stol);
-                const uint64_t kb = __ballot(kc);
-                if (mine) {
-                    if (ic) ic[10] += 1u;
-                    const uint32_t kept = (uint32_t)(kb >> (4 * rk)) & 15u;
-                    if (kept) {
-                        const int j = lowest_bit(kept);
-                        pend |= (kept & ~(1u << j)) << (4 * d);
-                        pos = 4 * pos + j;
-                        ++d;
-                    } else {
-                        live = resume();
-                    }
-                }
-            }
-            share(__ballot(live));
-        }
-#else
 #if WOST_TREE_SHARE_DESCENT
         for (;;) {
             const bool down = live && d < t.depth;
@@ -618,7 +560,6 @@ __device__ __forceinline__ Hit intersect_polylines_tree_wave(const SegTree& t, f
             share(__ballot(live));
 #endif
         }
-#endif
         const int s0 = pos * t.leaf;
         const int s1 = s0 + t.leaf < nseg ? s0 + t.leaf : nseg;
         if (ic && __any(live && s0 < s1)) ic[13] += 1u;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 4, session 23: quad-cooperative ray visits (WOST_JIT_TREE_QUAD=1: one child test
 # per lane, 16 visits per batch) against the per-lane visits -- bits, C5 tests, rates.
+# (The quad variant exists only in commit c799ffa; profiles/r04_ab/c5_quad_ray_visits_ab.log.)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/r04s23
