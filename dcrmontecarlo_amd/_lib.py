@@ -27,6 +27,7 @@ WOST_COMM_ID_BYTES = 128
 WOST_COMM_SUM, WOST_COMM_MAX = 0, 1
 WOST_BLOCK_WALKS = 4096
 WOST_MAX_SOURCES = 16   # include/wost.h
+WOST_TRIG = {"auto": 0, "exact": 1, "fast": 2}   # include/wost.h wost_trig
 WOST_SAMPLER_TABLE_N = 4097
 COMPAT = {"reference": 0, "fixed": 1}
 SLOT_BOUNDARY, SLOT_SOURCE = 0, 1
@@ -67,7 +68,8 @@ class WostTiming(ctypes.Structure):
 
 
 class WostDistTiming(ctypes.Structure):
-    _fields_ = [("local", WostTiming), ("walk_begin", c_int64), ("walk_end", c_int64), ("total_steps", c_uint64)]
+    _fields_ = [("local", WostTiming), ("walk_begin", c_int64), ("walk_end", c_int64), ("total_steps", c_uint64),
+                ("local_ms", c_double), ("agree_ms", c_double), ("gather_ms", c_double), ("merge_ms", c_double)]
 
 
 DIST_PREPARE = ctypes.CFUNCTYPE(c_int32, c_void_p, c_int64)
@@ -135,11 +137,13 @@ def _load():
         "wost_distributed_run": (c_int32, [POINTER(WostDistOps), c_int32, c_int32, c_int64, c_int64, c_int32,
                                            POINTER(c_double), POINTER(c_int64), POINTER(c_int64),
                                            POINTER(c_uint64)]),
+        "wost_dist_last_phases": (c_int32, [POINTER(c_double)]),
         "wost_dist_solve_key": (c_int32, [c_uint64, c_float, c_int32, POINTER(c_float), c_int64, POINTER(c_double)]),
         "wost_greens_norm": (c_int32, [c_double, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_screened_sample_fixed": (c_int32, [POINTER(c_float), POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_screened_cdf_fixed": (c_int32, [c_double, POINTER(c_double), c_int64, POINTER(c_double)]),
         "wost_set_jit": (c_int32, [H, c_int32]),
+        "wost_set_trig": (c_int32, [H, c_int32]),
         "wost_set_fixed_step_check": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
         "wost_kernel_source": (c_int32, [POINTER(WostProblem), ctypes.c_char_p, c_int64, POINTER(c_int64)]),

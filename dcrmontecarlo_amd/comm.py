@@ -11,8 +11,9 @@ The only thing libwost needs from outside is the 128-byte RCCL unique id, made o
 rank and handed to the others. ``Communicator.from_env`` does it without PyTorch: rank 0
 hosts a small key-value store on MASTER_ADDR:MASTER_PORT (:class:`SocketStore`, the
 standard library's sockets); under torchrun, whose elastic agent already listens on
-MASTER_PORT, the ranks of one node meet in a file named after their common parent (the
-agent) instead, and only a multi-node torchrun job uses torch's TCPStore client.
+MASTER_PORT, the ranks of one node meet in a file named after the launch's own values
+(MASTER_ADDR, MASTER_PORT, TORCHELASTIC_RUN_ID, restart count) instead, and only a
+multi-node torchrun job uses torch's TCPStore client.
 ``from_torch`` takes an initialised torch.distributed group, ``from_file`` a file every
 rank can read.
 """
@@ -32,12 +33,20 @@ import numpy as np
 from . import _lib
 
 
+_MAX_KEY, _MAX_VALUE = 1024, 4096      # the store carries ids (128 B) and short flags
+
+
 class _StoreHandler(socketserver.StreamRequestHandler):
     """One client connection: requests b"S" key value (set) and b"G" key (get, waits
-    until the key is set); keys and values are length-prefixed (u32, big endian)."""
+    until the key is set); keys and values are length-prefixed (u32, big endian), keys
+    at most 1 KiB and values 4 KiB (a longer prefix ends the connection). A key is set
+    once: a second b"S" of it is refused (b"\x01"), so no peer can replace an id that
+    rank 0 published."""
 
-    def _read(self):
+    def _read(self, cap):
         n = struct.unpack(">I", self.rfile.read(4))[0]
+        if n > cap:
+            raise OSError(f"store: field of {n} bytes exceeds {cap}")
         return self.rfile.read(n)
 
     def handle(self):
@@ -52,13 +61,15 @@ class _StoreHandler(socketserver.StreamRequestHandler):
             op = self.rfile.read(1)
             if not op:
                 return
-            key = self._read()
+            key = self._read(_MAX_KEY)
             if op == b"S":
-                val = self._read()
+                val = self._read(_MAX_VALUE)
                 with st.cond:
-                    st.kv[key] = val
-                    st.cond.notify_all()
-                self.wfile.write(b"\x00")
+                    fresh = key not in st.kv
+                    if fresh:
+                        st.kv[key] = val
+                        st.cond.notify_all()
+                self.wfile.write(b"\x00" if fresh else b"\x01")
             elif op == b"G":
                 with st.cond:
                     ok = st.cond.wait_for(lambda: key in st.kv or st.closed, timeout=st.timeout)
@@ -79,15 +90,17 @@ class _StoreServer(socketserver.ThreadingTCPServer):
 class SocketStore:
     """A minimal key-value store over TCP (standard library only) for the communicator's
     id: rank 0 hosts it (``is_master``), every rank -- rank 0 too -- is a client. ``get``
-    blocks until the key is set or ``timeout`` passes. The host keeps serving until
-    ``close`` (the communicator holds its store for its lifetime)."""
+    blocks until the key is set or ``timeout`` passes; keys are set once. The host listens
+    on ``host`` itself (MASTER_ADDR: loopback for bench.py's own launch), not on every
+    interface, and keeps serving until ``close`` (the communicator holds its store for
+    its lifetime)."""
 
     def __init__(self, host: str, port: int, is_master: bool, timeout: float = 300.0):
         self.timeout = float(timeout)
         self._srv = self._f = self._sock = None
         if is_master:
             self.kv, self.cond, self.closed = {}, threading.Condition(), False
-            self._srv = _StoreServer(("", int(port)), _StoreHandler)
+            self._srv = _StoreServer((host, int(port)), _StoreHandler)
             self._srv.store = self
             threading.Thread(target=self._srv.serve_forever, daemon=True).start()
         t0 = time.time()
@@ -109,7 +122,10 @@ class SocketStore:
     def set(self, key: str, value: bytes):
         self._f.write(b"S" + self._lp(key.encode()) + self._lp(bytes(value)))
         self._f.flush()
-        if self._f.read(1) != b"\x00":
+        st = self._f.read(1)
+        if st == b"\x01":
+            raise KeyError(f"store: {key!r} is already set")
+        if st != b"\x00":
             raise ConnectionError("store: set failed")
 
     def get(self, key: str) -> bytes:
@@ -142,11 +158,13 @@ class SocketStore:
 
 
 class _FileStore:
-    """Rank 0 publishes the id in a file named after the ranks' common parent process
-    (torchrun's agent on this node) and the launch's port, in a directory private to
-    this user, and the others wait for it; the
-    file is removed when rank 0's communicator closes (every rank has read it by then:
-    ncclCommInitRank is collective)."""
+    """Rank 0 publishes the id in a file named after values every rank of the launch
+    shares (``tag``: MASTER_ADDR, MASTER_PORT -- the agent's store listens there, so the
+    port is unique per live job on the node --, TORCHELASTIC_RUN_ID and the restart
+    count), in a directory private to this user, and the others wait for it. The file is
+    removed when rank 0's communicator closes (every rank has read it by then:
+    ncclCommInitRank is collective). A file older than this process's start (less a
+    minute of launch skew) is a crashed job's leftover and is not read."""
 
     def __init__(self, tag: str, rank: int, timeout: float):
         # a directory only this user can write, so no other user can plant an id there
@@ -156,6 +174,7 @@ class _FileStore:
         if st.st_uid != os.getuid() or (st.st_mode & 0o022):
             raise PermissionError(f"{d} is not a private directory of this user")
         self.dir, self.tag, self.rank, self.timeout, self.paths = d, tag, rank, timeout, []
+        self.not_before = _process_start_time() - 60.0
 
     def _path(self, key: str) -> str:
         safe = "".join(c if c.isalnum() else "_" for c in key)
@@ -175,11 +194,13 @@ class _FileStore:
         while True:
             try:
                 with open(path, "rb") as f:
-                    return f.read()
+                    if os.fstat(f.fileno()).st_mtime >= self.not_before:
+                        return f.read()
             except OSError:
-                if time.time() - t0 > self.timeout:
-                    raise TimeoutError(f"no communicator id in {path} after {self.timeout} s") from None
-                time.sleep(0.02)
+                pass
+            if time.time() - t0 > self.timeout:
+                raise TimeoutError(f"no communicator id in {path} after {self.timeout} s")
+            time.sleep(0.02)
 
     def close(self):
         for p in self.paths:
@@ -188,6 +209,24 @@ class _FileStore:
             except OSError:
                 pass
         self.paths = []
+
+
+def _process_start_time() -> float:
+    """This process's start (wall clock, s); now if it cannot be read."""
+    try:
+        import psutil
+
+        return float(psutil.Process().create_time())
+    except Exception:   # psutil missing or refused: no staleness test beyond the tag
+        return time.time()
+
+
+def _launch_tag() -> str:
+    """The file store's name for this launch: values every rank of it shares (not the
+    parent pid -- a rank may sit below a wrapper of its own)."""
+    parts = [os.environ.get("MASTER_ADDR", ""), os.environ.get("MASTER_PORT", "0"),
+             os.environ.get("TORCHELASTIC_RUN_ID", ""), os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")]
+    return ".".join("".join(c if c.isalnum() else "_" for c in p) for p in parts)
 
 
 def launch_store(timeout: float = 300.0):
@@ -199,9 +238,8 @@ def launch_store(timeout: float = 300.0):
     if not agent:
         return SocketStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
                            is_master=(rank == 0), timeout=timeout)
-    if int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == world:   # one node: the ranks share the agent as parent
-        tag = f"{os.getppid()}.{os.environ.get('MASTER_PORT', '0')}.{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}"
-        return _FileStore(tag, rank, timeout)
+    if int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == world:   # one node: a file on it
+        return _FileStore(_launch_tag(), rank, timeout)
     from datetime import timedelta
 
     import torch.distributed as dist
@@ -347,7 +385,9 @@ def _distributed_sums(solver, comm: Communicator, p: np.ndarray, nWalks: int, ma
                                                float(eps), int(seed) & (2**64 - 1), _lib.dptr(sums), ctypes.byref(t)),
                "wost_solve_distributed", comm=True)
     timing = {k: getattr(t.local, k) for k, _ in _lib.WostTiming._fields_}
-    timing.update({"walk_begin": int(t.walk_begin), "walk_end": int(t.walk_end), "all_steps": int(t.total_steps)})
+    timing.update({"walk_begin": int(t.walk_begin), "walk_end": int(t.walk_end), "all_steps": int(t.total_steps),
+                   "local_ms": float(t.local_ms), "agree_ms": float(t.agree_ms), "gather_ms": float(t.gather_ms),
+                   "merge_ms": float(t.merge_ms)})
     solver.last_timing = timing
     solver.last_point_sums = sums
     return sums, timing

@@ -190,6 +190,7 @@ struct wost_handle {
 
     // compat="fixed" delta tracking: refuse solves whose walks would all hit maxSteps
     bool fixed_step_check = true;
+    int trig_mode = WOST_TRIG_AUTO;       // wost_set_trig
 
     // field-specialised walk kernel (wost_jit.cpp)
     bool jit_enabled = true;
@@ -266,13 +267,22 @@ int upload_program(wost_handle* h) {
 // The field-specialised kernel for `mode` (with the walk recorder compiled in
 // when `record`), or nullptr when it is disabled or could not be built (the
 // precompiled kernel is used then; same results).
+// wost_set_trig's choice for this handle: WOST_TRIG_AUTO is exact for a Neumann polyline
+// of >= 3 segments (a curved boundary, where a direction's last ulp decides where the
+// walk goes), the hardware's sin/cos otherwise
+bool exact_trig_of(const wost_handle* h) {
+    if (h->trig_mode != WOST_TRIG_AUTO) return h->trig_mode == WOST_TRIG_EXACT;
+    return (int)(h->nverts.size() / 2) - 1 >= 3;
+}
+
 hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock,
                          bool global_polylines = false, int tree_stage = 0) {
     if (!h->jit_enabled) return nullptr;
-    // the cache key holds everything the source depends on: the staging level and the
-    // exact workgroup size (a multiple of 64, at most 1024)
-    const int key = ((((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 3 + tree_stage) * 17 +
-                     block / 64) * 2 + (global_polylines ? 1 : 0);
+    // the cache key holds everything the source depends on: the staging level, the
+    // exact workgroup size (a multiple of 64, at most 1024) and the trig choice
+    const bool exact = exact_trig_of(h);
+    const int key = (((((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 3 + tree_stage) * 17 +
+                      block / 64) * 2 + (global_polylines ? 1 : 0)) * 2 + (exact ? 1 : 0);
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
     h->jit_alpha_fn = nullptr;
@@ -287,7 +297,7 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
     }
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
                                          (int)(h->dverts.size() / 2), h->nverts.data(), nn, record, ns, block,
-                                         phi.empty() ? nullptr : phi.data(), global_polylines, tree_stage);
+                                         phi.empty() ? nullptr : phi.data(), global_polylines, tree_stage, exact);
     std::string err;
     hipFunction_t fn = nullptr;
     hipFunction_t afn = nullptr;
@@ -561,6 +571,9 @@ int create_host(const wost_problem* pb, wost_handle** out) {
     h->compat = pb->compat;
     if (const char* e = std::getenv("WOST_JIT")) h->jit_enabled = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("WOST_TREE_MIN_SEGMENTS")) h->tree_min_segments = std::atoi(e);
+    if (const char* e = std::getenv("WOST_TRIG"))
+        h->trig_mode = std::strcmp(e, "exact") == 0 ? WOST_TRIG_EXACT : std::strcmp(e, "fast") == 0 ? WOST_TRIG_FAST
+                                                                                                   : WOST_TRIG_AUTO;
     if (const char* e = std::getenv("WOST_TREE_LEAF")) h->tree_leaf = std::min(32, std::max(1, std::atoi(e)));
     // solvers/WoStSolver.py:54-64: any of sigma/alpha turns on delta tracking,
     // the missing one defaults to sigma = 0 / alpha = 1 (constant => Q9 fallback).
@@ -635,10 +648,19 @@ int wost_create(const wost_problem* pb, wost_handle** out) {
     if (!h->nverts.empty()) {
         CREATE_TRY(hipMalloc(&h->d_nverts, sizeof(float) * h->nverts.size()));
         CREATE_TRY(hipMemcpy(h->d_nverts, h->nverts.data(), sizeof(float) * h->nverts.size(), hipMemcpyHostToDevice));
+        // atan2 of each segment's left normal (:227-228, quirk Q2) on the host: the C
+        // library's atan2f is what torch.atan2 of the reference's 0-d tensors calls, and
+        // the device's atan2f differs from it on ~half of the C5 topography's segments
+        // (tools/r05/trig_compare.py), each a different direction after a Neumann hit
         const int nseg = (int)(h->nverts.size() / 2) - 1;
-        CREATE_TRY(hipMalloc(&h->d_seg_phi, sizeof(float) * std::max(nseg, 1)));
-        CREATE_TRY(launch_segment_phi(h->d_nverts, nseg, h->d_seg_phi, h->stream));
-        CREATE_TRY(hipStreamSynchronize(h->stream));
+        std::vector<float> phi((size_t)std::max(nseg, 1), 0.0f);
+        for (int i = 0; i < nseg; ++i) {
+            const float2 a{h->nverts[2 * i], h->nverts[2 * i + 1]}, b{h->nverts[2 * i + 2], h->nverts[2 * i + 3]};
+            const float2 n = segment_left_normal(a, b);
+            phi[i] = std::atan2(n.y, n.x);
+        }
+        CREATE_TRY(hipMalloc(&h->d_seg_phi, sizeof(float) * phi.size()));
+        CREATE_TRY(hipMemcpy(h->d_seg_phi, phi.data(), sizeof(float) * phi.size(), hipMemcpyHostToDevice));
     }
 #undef CREATE_TRY
     if ((rc = upload_program(h)) != WOST_OK) {
@@ -930,6 +952,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     a.inv_walks_per_point = 1.0 / (double)W;
     a.rec = d_rec;
     a.rec_stride = (int32_t)rec_stride;
+    a.exact_trig = exact_trig_of(h) ? 1 : 0;
     if (mode_tree(mode)) {
         a.tree = reinterpret_cast<const float4*>(h->d_tree);
         a.tree_first_leaf = h->tree.first_leaf;
@@ -1256,7 +1279,7 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
     }
     const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
                                          (int)(h->dverts.size() / 2), h->nverts.data(), nn, false, 1, block,
-                                         phi.empty() ? nullptr : phi.data(), false, stage);
+                                         phi.empty() ? nullptr : phi.data(), false, stage, exact_trig_of(h));
     delete h;
     *length = (int64_t)src.size();
     if (out && capacity > 0) {
@@ -1275,6 +1298,16 @@ int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_seg
         h->tree_leaf = leaf_segments;
         h->tree_ready = false;
     }
+    return WOST_OK;
+}
+
+int wost_set_trig(wost_handle* h, int32_t mode) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    if (mode != WOST_TRIG_AUTO && mode != WOST_TRIG_EXACT && mode != WOST_TRIG_FAST)
+        return fail(WOST_ERR_INVALID_ARG, "trig mode must be WOST_TRIG_AUTO, _EXACT or _FAST");
+    h->trig_mode = mode;
+    h->jit_fn = nullptr;
+    h->jit_mode = -1;
     return WOST_OK;
 }
 

@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -17,6 +18,18 @@
 namespace {
 
 thread_local std::string g_comm_err;
+// wall-clock phases of this thread's last wost_distributed_run (wost_dist_last_phases)
+thread_local double g_phases[4] = {0.0, 0.0, 0.0, 0.0};
+
+struct PhaseClock {
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    double lap() {   // ms since the last lap
+        const auto now = std::chrono::steady_clock::now();
+        const double ms = std::chrono::duration<double, std::milli>(now - t).count();
+        t = now;
+        return ms;
+    }
+};
 
 int cfail(int code, const char* fmt, ...) {
     char buf[512];
@@ -229,9 +242,17 @@ int wost_dist_solve_key(uint64_t seed, float eps, int32_t max_steps, const float
     return WOST_OK;
 }
 
+int wost_dist_last_phases(double* ms) {
+    if (!ms) return cfail(WOST_ERR_INVALID_ARG, "NULL argument");
+    for (int i = 0; i < 4; ++i) ms[i] = g_phases[i];
+    return WOST_OK;
+}
+
 int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank, int64_t n_points,
                          int64_t walks_per_point, int32_t row, double* point_stats, int64_t* walk_begin,
                          int64_t* walk_end, uint64_t* total_steps) {
+    for (double& v : g_phases) v = 0.0;
+    PhaseClock clk;
     if (!ops || !ops->allreduce || !ops->allgather || n_ranks < 1 || rank < 0 || rank >= n_ranks)
         return cfail(WOST_ERR_INVALID_ARG, "wost_distributed_run: no transport or bad rank %d of %d", rank, n_ranks);
     // Every rank reaches the same two collectives, whatever fails locally: the
@@ -285,17 +306,26 @@ int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank
         local = WOST_ERR_INVALID_ARG;
         local_msg = "bad agreement key";
     }
+    // a NaN key entry (e.g. eps) fails this rank, and through the failure flag every rank:
+    // NaN compares unequal to itself, so it cannot be agreed on
+    for (int k = 0; k < nk && local == WOST_OK; ++k)
+        if (!(ops->key[k] == ops->key[k])) {
+            local = WOST_ERR_INVALID_ARG;
+            local_msg = "NaN in the solve's arguments (agreement key)";
+        }
     double agree[9 + 2 * WOST_DIST_MAX_KEY] = {local != WOST_OK ? 1.0 : 0.0, (double)n_points, -(double)n_points,
                                                (double)row, -(double)row, (double)walks_per_point,
                                                -(double)walks_per_point, (double)nk, -(double)nk};
     for (int k = 0; k < nk; ++k) {
-        // NaN never agrees: map it to a value no finite key takes
-        const double v = ops->key[k] == ops->key[k] ? ops->key[k] : 1e308;
+        // (a NaN entry already failed this rank above; 0 keeps the reduction finite)
+        const double v = ops->key[k] == ops->key[k] ? ops->key[k] : 0.0;
         agree[9 + 2 * k] = v;
         agree[10 + 2 * k] = -v;
     }
     const int na = 9 + 2 * WOST_DIST_MAX_KEY;   // fixed length: every rank reduces the same count
+    g_phases[0] = clk.lap();
     int rc = ops->allreduce(ops->ctx, agree, na, WOST_COMM_MAX);
+    g_phases[1] = clk.lap();
     if (rc != WOST_OK) return cfail(rc, "agreement all-reduce: %s", g_comm_err.c_str());
     if (local != WOST_OK) return cfail(local, "rank %d: %s", rank, local_msg.c_str());
     if (agree[0] > 0.0) return cfail(WOST_ERR_COMM, "rank %d: another rank failed; no result", rank);
@@ -311,7 +341,9 @@ int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank
         rc = ops->allgather(ops->ctx, mine.data(), (int64_t)per_rank, all.data());
         if (rc != WOST_OK) return cfail(rc, "block all-gather: %s", g_comm_err.c_str());
     }
+    g_phases[2] = clk.lap();
     rc = wost_shard_merge(all.data(), n_points, walks_per_point, n_ranks, row, point_stats);
+    g_phases[3] = clk.lap();
     if (rc != WOST_OK) return rc;
     if (walk_begin) *walk_begin = w0;
     if (walk_end) *walk_end = w1;
@@ -392,6 +424,10 @@ int wost_solve_distributed(wost_handle* h, wost_comm* c, const float* points, in
         timing->walk_begin = w0;
         timing->walk_end = w1;
         timing->total_steps = steps;
+        timing->local_ms = g_phases[0];
+        timing->agree_ms = g_phases[1];
+        timing->gather_ms = g_phases[2];
+        timing->merge_ms = g_phases[3];
     }
     return WOST_OK;
 }

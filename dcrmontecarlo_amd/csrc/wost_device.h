@@ -159,6 +159,49 @@ WOST_HD float f_cos(float x) { return cosf(x); }
 WOST_HD float f_log(float x) { return logf(x); }
 #endif
 
+// The walk direction's cos and sin (:230-232), correctly rounded to float32: the
+// reference's torch.cos/torch.sin round the exact values to float32 (MKL's vector
+// functions, within an ulp), and a one-ulp change of a direction changes ~20% of the C5
+// walks (tests/test_c5_reference.py), so the hardware v_sin/v_cos (tens of ulps near
+// the zeros) and even OCML's sinf/cosf (1 ulp on 13-21% of the walk angles,
+// tools/r05/trig_compare.py) leave the reference's walks. Evaluated in double: k =
+// rint(x 2/pi); r = x - k pi/2 with pi/2 in two parts (k P1 and x - k P1 are exact for
+// |k| < 2^20: Sterbenz), then fdlibm's kernel polynomials on |r| <= pi/4 (< 1 double
+// ulp), rounded once to float32. That differs from the correctly rounded result only
+// when the exact value lies within ~2^-52 relative of a float32 rounding boundary
+// (~1e-8 of the angles; tests/test_trig_rn.py compares every angle :226 can draw with
+// the C library's double cos/sin rounded to float32). |x| >= 2^20 (never a walk angle:
+// |theta| < 3 pi) takes the library functions.
+WOST_HD void sincos_rn(float xf, float& s_out, float& c_out) {
+#pragma clang fp contract(off)
+    const double x = (double)xf;
+    if (!(__builtin_fabs(x) < 1048576.0)) {   // also NaN / inf
+        s_out = sinf(xf);
+        c_out = cosf(xf);
+        return;
+    }
+    const double P1 = 1.57079632673412561417e+00;    // 0x3FF921FB54400000: pi/2, 33 bits
+    const double P1T = 6.07710050650619224932e-11;   // pi/2 - P1
+    const double k = __builtin_rint(x * 6.36619772367581382433e-01);
+    const double r = __builtin_fma(-k, P1T, x - k * P1);
+    const double z = r * r;
+    const double sp = -1.66666666666666324348e-01 +
+                      z * (8.33333333332248946124e-03 +
+                           z * (-1.98412698298579493134e-04 +
+                                z * (2.75573137070700676789e-06 +
+                                     z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10))));
+    const double cp = 4.16666666666666019037e-02 +
+                      z * (-1.38888888888741095749e-03 +
+                           z * (2.48015872894767294178e-05 +
+                                z * (-2.75573143513906633035e-07 +
+                                     z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11))));
+    const float s = (float)(r + (r * z) * sp);
+    const float c = (float)((1.0 - 0.5 * z) + (z * z) * cp);
+    const int q = (int)(int64_t)k & 3;
+    s_out = q == 0 ? s : q == 1 ? c : q == 2 ? -s : -c;
+    c_out = q == 0 ? c : q == 1 ? -s : q == 2 ? -c : s;
+}
+
 // The correctly rounded square root (sqrtf under -fhip-fp32-correctly-rounded-
 // divide-sqrt) of a distance. The compiler's sequence is v_sqrt_f32 of x
 // (scaled by 2^32 below 2^-96), both neighbours s -+ 1 ulp tested by their

@@ -35,8 +35,9 @@ namespace {
 // unit_direction. Ablations (timing studies only: the results are WRONG, the
 // walks merely stay statistically alike): 4 a cheap hash instead of Philox, 8 no
 // alpha(z) evaluation, 16 no sigma' at collisions, 32 no Neumann ray query;
-// 64 compiled-in silhouette scans unrolled by 4 only, 128 the device library's
-// accurate sinf/cosf for the step direction instead of v_sin/v_cos; 512 no
+// 64 compiled-in silhouette scans unrolled by 4 only, 128 the device library's sinf/cosf
+// instead of v_sin/v_cos when the handle's directions use the hardware trig
+// (wost_set_trig); 512 no
 // whole-field saturation shortcut in the alpha jet (jet_body); 1024 compiled-in
 // Neumann ray scans unrolled by 2 instead of fully; 2048 sqrtf instead of
 // sqrt_rn for the distances; 4096 the tree's ray query
@@ -382,7 +383,8 @@ bool jit_const_neumann(int mode, int nn) {
 
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources,
-                         int block, const float* seg_phi, bool global_polylines, int tree_stage) {
+                         int block, const float* seg_phi, bool global_polylines, int tree_stage,
+                         bool exact_trig) {
     const bool neu = mode_neu(mode);
     const bool src = mode_src(mode);
     const bool delta = mode_delta(mode);
@@ -401,6 +403,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 65536) o << "#define WOST_ABL_NO_SILHOUETTE 1\n";
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
+    o << "#define WOST_JIT_TRIG_EXACT " << (exact_trig ? 1 : 0) << "\n";   // wost_set_trig
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
     if (const char* e = std::getenv("WOST_JIT_PHILOX_AHEAD"))   // A/B: Philox one step ahead
         o << "#define WOST_PHILOX_AHEAD " << std::max(0, std::min(3, std::atoi(e))) << "\n";

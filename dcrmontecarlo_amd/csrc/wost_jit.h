@@ -43,7 +43,7 @@ bool jit_const_neumann(int mode, int nn);
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record,
                          int n_sources = 1, int block = 256, const float* seg_phi = nullptr,
-                         bool global_polylines = false, int tree_stage = 0);
+                         bool global_polylines = false, int tree_stage = 0, bool exact_trig = true);
 
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.

@@ -361,23 +361,6 @@ wost_eval_field_kernel(const char* prog, int which, const float2* __restrict__ p
     }
 }
 
-// atan2 of each Neumann segment's left normal: the rotation the walk applies
-// after a hit on that segment (solvers/WoStSolver.py:227-228), computed once
-// with the same device functions the walk used to evaluate per step.
-__global__ void __launch_bounds__(256)
-wost_segment_phi_kernel(const float2* __restrict__ verts, int nseg, float* __restrict__ phi) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nseg) return;
-    const float2 n = segment_left_normal(verts[i], verts[i + 1]);
-    phi[i] = atan2f(n.y, n.x);
-}
-
-hipError_t launch_segment_phi(const float2* verts, int nseg, float* phi, hipStream_t s) {
-    if (nseg <= 0) return hipSuccess;
-    wost_segment_phi_kernel<<<(nseg + 255) / 256, 256, 0, s>>>(verts, nseg, phi);
-    return hipGetLastError();
-}
-
 hipError_t launch_eval_field(const char* prog, int which, const float2* pts, int64_t n,
                              float4* out, hipStream_t s) {
     if (n <= 0) return hipSuccess;

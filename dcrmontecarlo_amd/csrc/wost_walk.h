@@ -81,7 +81,8 @@ struct WalkArgs {
     float4 pool_box;
     int32_t pool_near_waves;     // the workgroup's first pool_near_waves waves take the near walks
                                  // (0: each wave takes the class most of its walks are in)
-    int32_t pool_pad;
+    int32_t exact_trig;          // precompiled kernels: the direction's cos/sin correctly rounded
+                                 // (wost_set_trig; the field-specialised kernels fix it at compile time)
 };
 
 // words of one parked walk: global id (2), local index (2), x, y, dD, step | onB << 31,
@@ -689,8 +690,12 @@ __device__ __forceinline__ bool pool_near(float4 b, float x, float y) {
 }
 // walks parked in class c (header word 1 + c), read with an atomic load so that every
 // read goes to memory (under the lock: exact; outside it: a hint)
+// A pool count as a wave-uniform value: the first active lane's load, broadcast. The
+// callers branch on it around pool_lock/pool_unlock, which must run with the whole wave
+// (lane 0 takes the lock for it), so no lane may see a different count.
 __device__ __forceinline__ uint32_t pool_count(uint32_t* pool, int c) {
-    return __hip_atomic_load(pool + 1 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(pool + 1 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 // the pool lock (header word 0), taken by the wave's first lane for the whole wave; the
 // fences order the wave's slot reads and writes inside it
@@ -710,6 +715,23 @@ __device__ __forceinline__ void pool_unlock(uint32_t* pool, int lane, uint32_t n
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) __hip_atomic_store(pool, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The direction's cos and sin (wost_set_trig): correctly rounded (sincos_rn, the
+// reference's values but for its own ulp errors; double-precision arithmetic) or the
+// hardware's v_sin/v_cos (a few ulps, tens near the zeros). The field-specialised kernels
+// fix the choice at compile time (WOST_JIT_TRIG_EXACT 1 / 0), the precompiled ones take
+// it per launch (a uniform branch).
+__device__ __forceinline__ void walk_sincos(float theta, float& sn, float& cs, bool exact) {
+#if defined(WOST_JIT_TRIG_EXACT)
+    exact = WOST_JIT_TRIG_EXACT != 0;
+#endif
+    if (exact) {
+        sincos_rn(theta, sn, cs);
+    } else {
+        cs = f_cos(theta);
+        sn = f_sin(theta);
+    }
 }
 
 #ifndef WOST_REFILL_MIN   // idle lanes that trigger a refill (tools/ab_refill.sh; 1 = every iteration)
@@ -1062,12 +1084,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #endif
             float theta = (u01(rn.x) * 2.0f) * kPiF;                 // :226
             // :227-228 (quirk Q2): atan2(normal) is a property of the segment that
-            // was hit, precomputed per segment with the same device atan2f
+            // was hit, precomputed per segment on the host (the C library's atan2f)
             if (NEU && onB) theta = FIX ? theta / 2.0f + (phi - kPiF / 2.0f) : theta / 2.0f + phi;
             onB0 = onB;
             phi0 = phi;
-            cs = f_cos(theta);                                       // :230-232
-            sn = f_sin(theta);
+            walk_sincos(theta, sn, cs, A.exact_trig != 0);           // :230-232
         };
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
@@ -1136,7 +1157,8 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             if constexpr (FIX && !DELTA) {                           // Q13 fixed: own direction
                 float ts = (u01(rn.w) * 2.0f) * kPiF;
                 if (NEU && onB0) ts = ts / 2.0f + (phi0 - kPiF / 2.0f);   // the inward hemisphere
-                const float cs2 = f_cos(ts), sn2 = f_sin(ts);
+                float cs2, sn2;
+                walk_sincos(ts, sn2, cs2, A.exact_trig != 0);
                 yx = px + rs * cs2;
                 yy = py + rs * sn2;
                 if (NEU)   // not visible

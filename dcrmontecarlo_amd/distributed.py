@@ -188,7 +188,7 @@ def solve_key(seed: int, eps: float, max_steps: int, points) -> np.ndarray:
 
 
 def run_protocol(n_ranks: int, rank: int, n_points: int, walks_per_point: int, row: int, solve_range, allreduce,
-                 allgather, prepare=None, key=None):
+                 allgather, prepare=None, key=None, phases: dict | None = None):
     """libwost's distributed protocol (wost_distributed_run: agreement all-reduce,
     all-gather of the padded block rows, ordered merge) over Python callables:
     solve_range(w0, w1) -> [n_points, blocks, row] float64 of this rank's walks;
@@ -197,7 +197,10 @@ def run_protocol(n_ranks: int, rank: int, n_points: int, walks_per_point: int, r
     hold identically; a rank that differs makes every rank raise ValueError.
     Returns (point sums [n_points, row], (walk_begin, walk_end), total walk-steps).
     Raises the local exception on the rank whose callback failed, WostError on the
-    others (no rank is left waiting in a collective)."""
+    others (no rank is left waiting in a collective). ``phases`` (a dict) receives the
+    protocol's wall-clock phases on this rank (wost_dist_last_phases): local_ms (the
+    local solve and pack), agree_ms (the agreement all-reduce: it waits for the slowest
+    rank), gather_ms and merge_ms."""
     from . import _lib
 
     tr = _Transport(n_points, row, solve_range, allreduce, allgather, prepare, n_ranks=n_ranks, key=key)
@@ -206,6 +209,10 @@ def run_protocol(n_ranks: int, rank: int, n_points: int, walks_per_point: int, r
     rc = _lib.lib.wost_distributed_run(ctypes.byref(tr.ops), int(n_ranks), int(rank), int(n_points),
                                        int(walks_per_point), int(row), _lib.dptr(out), ctypes.byref(w0),
                                        ctypes.byref(w1), ctypes.byref(steps))
+    if phases is not None:
+        ms = (ctypes.c_double * 4)()
+        _lib.lib.wost_dist_last_phases(ms)
+        phases.update(local_ms=ms[0], agree_ms=ms[1], gather_ms=ms[2], merge_ms=ms[3])
     if rc != _lib.WOST_OK and tr.error is not None:
         raise tr.error
     _lib.check(rc, "wost_distributed_run", comm=True)

@@ -281,6 +281,14 @@ class WostSolver_2D:
         kernel that interprets the fields. Both give identical results."""
         _lib.check(_lib.lib.wost_set_jit(self._h, 1 if enable else 0), "wost_set_jit")
 
+    def set_trig(self, mode: str = "auto"):
+        """The walk direction's cos/sin (wost_set_trig): "exact" correctly rounded (the
+        reference's torch values but for their own ulp errors), "fast" the hardware
+        sin/cos, "auto" (default) exact when the Neumann polyline has >= 3 segments."""
+        if mode not in _lib.WOST_TRIG:
+            raise ValueError(f"trig mode must be one of {sorted(_lib.WOST_TRIG)}, got {mode!r}")
+        _lib.check(_lib.lib.wost_set_trig(self._h, _lib.WOST_TRIG[mode]), "wost_set_trig")
+
     def set_fixed_step_check(self, enable: bool):
         """compat="fixed" delta tracking refuses (ValueError) a solve whose walks would all
         hit maxSteps (~d^2 sigma_bar / 4 steps from Dirichlet distance d at the median

@@ -18,6 +18,7 @@ data:
 from __future__ import annotations
 
 import math
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -237,6 +238,157 @@ def compare_to_replay(vm: np.ndarray, vh: np.ndarray, sm: np.ndarray, sh: np.nda
             "rho_a_gpu": [float(x) for x in g.rho_a]}
 
 
+@dataclass
+class WennerReplay:
+    """The reference's C5 Wenner survey replayed on libwost's Philox stream (tests/golden/
+    rho_replay_wenner_topography_physical.npz, tools/gen_fixtures.py --only c5_rho_replay):
+    setSourceTerm(transmitter q) + _solveUnified at both receivers (M, N) of each listed
+    quadripole, the physical conductivity and the alpha_bg background (the model's
+    sigma_bar), each receiver's walks carrying the ids and the seed they have in
+    run_wenner_survey(seed=survey_seed): walk w of electrode e has id (e - j0) W + w in
+    its group's launch, seed group_seed(survey_seed, g). Values and steps [Q, 2, W]."""
+    points: np.ndarray
+    quadripoles: np.ndarray      # [Q, 4] (A, M, N, B)
+    receivers: np.ndarray        # [Q, 2] electrodes M, N
+    groups: np.ndarray           # [Q, 2] their electrode group
+    n_walks: int
+    max_steps: int
+    eps: float
+    survey_seed: int
+    alpha_bg: float
+    width: float
+    sigma_bar: float
+    model_values: np.ndarray
+    background_values: np.ndarray
+    model_steps: np.ndarray
+    background_steps: np.ndarray
+
+
+def load_wenner_replay(path: str) -> WennerReplay | None:
+    try:
+        z = np.load(path, allow_pickle=False)
+    except OSError:
+        return None
+    return WennerReplay(z["points"], z["quadripoles"], z["receivers"], z["groups"], int(z["n_walks"]),
+                        int(z["max_steps"]), float(z["eps"]), int(z["survey_seed"]), float(z["alpha_bg"]),
+                        float(z["width"]), float(z["sigma_bar"]), z["model_values"], z["background_values"],
+                        z["model_steps"], z["background_steps"])
+
+
+def wenner_replay_subset(ref: WennerReplay, idx) -> WennerReplay:
+    """The replay restricted to the quadripoles ``idx`` (a smaller CPU check)."""
+    import dataclasses
+
+    idx = np.asarray(idx)
+    return dataclasses.replace(ref, quadripoles=ref.quadripoles[idx], receivers=ref.receivers[idx],
+                               groups=ref.groups[idx], model_values=ref.model_values[idx],
+                               background_values=ref.background_values[idx], model_steps=ref.model_steps[idx],
+                               background_steps=ref.background_steps[idx])
+
+
+def wenner_replay_walks(ref: WennerReplay, solve_walks, a: int = 1):
+    """Per-walk values and steps [Q, 2, W] of the replay's receivers for the model (field
+    0) and the background (field 1), from ``solve_walks(field, points, sources, W, seed,
+    rows) -> (values [S, n, W], steps [n, W])`` run per electrode group exactly as
+    run_wenner_survey launches it: the group's electrodes, its seed, the transmitters
+    the listed quadripoles need there (one launch per group and field). ``rows`` are the
+    group's electrodes (local indices) whose walks are read: a solver may skip the others."""
+    E = len(ref.points)
+    batches = list(wenner_batches(E, a))
+    Q, W = len(ref.quadripoles), ref.n_walks
+    out = [np.zeros((Q, 2, W)), np.zeros((Q, 2, W)), np.zeros((Q, 2, W), np.int64), np.zeros((Q, 2, W), np.int64)]
+    for g in sorted(set(int(x) for x in ref.groups.ravel())):
+        j0, j1, _, _ = batches[g]
+        need = [(i, k) for i in range(Q) for k in range(2) if int(ref.groups[i, k]) == g]
+        tx = sorted(set(int(ref.quadripoles[i, 0]) for i, _ in need))
+        srcs = [dipole_source(ref.points[q], ref.points[q + 3 * a], ref.width) for q in tx]
+        rows = sorted(set(int(ref.receivers[i, k]) - j0 for i, k in need))
+        for f in (0, 1):
+            v, st = solve_walks(f, ref.points[j0:j1], srcs, W, group_seed(ref.survey_seed, g), rows)
+            for i, k in need:
+                e = int(ref.receivers[i, k]) - j0
+                out[f][i, k] = v[tx.index(int(ref.quadripoles[i, 0])), e]
+                out[2 + f][i, k] = st[e]
+    return tuple(out)
+
+
+def solver_replay_walks(model_solver, background_solver, ref: WennerReplay):
+    """wenner_replay_walks' solver on the device: the group's multi-source launch on the
+    model or background handle (WostSolver_2D.solve_sources_walks), as the survey runs it."""
+    def solve_walks(f, pts, srcs, W, seed, rows):
+        s = (model_solver, background_solver)[f]
+        return s.solve_sources_walks(pts, srcs, nWalks=W, maxSteps=ref.max_steps, eps=ref.eps, seed=seed)
+
+    return solve_walks
+
+
+def compare_wenner_replay(vm, vh, sm, sh, ref: WennerReplay, k_sigma: float = 4.0) -> dict:
+    """rho_a parity of the C5 Wenner survey against the reference replayed on the same
+    walks. C5's walks are chaotic: a last-ulp difference at a Neumann hit (the reference's
+    torch cos/sin and 10k-element reductions round a few per cent of their results one ulp
+    off the correctly rounded value) sends a walk elsewhere, so a few per cent of the walks
+    leave the reference's path and end with an unrelated value. Each quadripole's rho_a
+    difference comes from those walks alone, and is bounded by them: |drho| <= k_sigma *
+    sigma_chaos + 1e-5 |rho|, sigma_chaos the delta-method error of rho_a over only the
+    diverged walks (each a difference of two draws of the walk's distribution: 2 var per
+    walk), plus what the identical walks may differ by (1e-3 of each value: the walk
+    identity test's tolerance) and 1e-5 |rho|."""
+    rb = 1.0 / ref.alpha_bg
+    W = ref.n_walks
+    rm, rh = np.asarray(ref.model_values, np.float64), np.asarray(ref.background_values, np.float64)
+    vm, vh = np.asarray(vm, np.float64), np.asarray(vh, np.float64)
+    scale_m, scale_h = max(np.abs(rm).max(), 1e-300), max(np.abs(rh).max(), 1e-300)
+    same_m = (np.asarray(sm) == ref.model_steps) & (np.abs(vm - rm) <= 1e-3 * np.abs(rm) + 1e-5 * scale_m)
+    same_h = (np.asarray(sh) == ref.background_steps) & (np.abs(vh - rh) <= 1e-3 * np.abs(rh) + 1e-5 * scale_h)
+    div = ~(same_m & same_h)                                  # [Q, 2, W]
+
+    def rho(m, h):
+        A, B = m[:, 0].mean(1) - m[:, 1].mean(1), h[:, 0].mean(1) - h[:, 1].mean(1)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return rb * A / B, A, B
+
+    g, Ag, _ = rho(vm, vh)
+    r, A, B = rho(rm, rh)
+    nd = div.sum(2)                                           # [Q, 2] diverged walks per receiver
+    var_m, var_h = rm.var(2, ddof=1), rh.var(2, ddof=1)       # [Q, 2] walk-value variance per receiver
+    with np.errstate(divide="ignore", invalid="ignore"):
+        R = r / rb
+        sig_a = np.sqrt((2.0 * nd * var_m).sum(1) / (W * W))   # dV(model) over the diverged walks
+        sig = rb / np.abs(B) * np.sqrt(((2.0 * nd * var_m).sum(1) + R * R * (2.0 * nd * var_h).sum(1)) / (W * W))
+        rel = np.abs(g - r) / np.abs(r)
+        rel_a = np.abs(Ag - A) / np.abs(A)
+        # the walks that did not diverge agree within the per-walk tolerance above
+        e_m = ((1e-3 * np.abs(rm) + 1e-5 * scale_m) * ~div).sum(2).sum(1) / W
+        e_h = ((1e-3 * np.abs(rh) + 1e-5 * scale_h) * ~div).sum(2).sum(1) / W
+        tol = k_sigma * np.nan_to_num(sig) + rb / np.abs(B) * (e_m + np.abs(R) * e_h) + 1e-5 * np.abs(r)
+    ok = np.abs(g - r) <= tol
+    ok_a = np.abs(Ag - A) <= k_sigma * sig_a + e_m + 1e-5 * np.abs(A)
+    clean = nd.sum(1) == 0
+    return {"fixture": "tests/golden/rho_replay_wenner_topography_physical.npz (reference setSourceTerm + "
+                       "_solveUnified on the Philox stream)",
+            "quadripoles": int(len(r)), "walks_per_receiver": int(W),
+            "walks_identical": float(1.0 - div.mean()),
+            "steps_identical": float(np.mean(np.concatenate([(np.asarray(sm) == ref.model_steps).ravel(),
+                                                              (np.asarray(sh) == ref.background_steps).ravel()]))),
+            "quadripoles_without_diverged_walks": int(clean.sum()),
+            "rel_diff_max_without_diverged_walks": {"rho_a": float(np.max(rel[clean])), "dv_model": float(np.max(
+                rel_a[clean]))} if clean.any() else None,
+            "tolerance": f"|d| <= {k_sigma} sigma_chaos + the identical walks' 1e-3 tolerance + 1e-5 |value| "
+                         "(sigma_chaos: the delta-method error of the value over the diverged walks only)",
+            "all_within_tolerance": bool(ok.all() and ok_a.all()),
+            "rho_a": {"within_tolerance": int(ok.sum()),
+                      "max_d_over_sigma_chaos": float(np.max(np.where(sig > 0, np.abs(g - r) / np.where(sig > 0, sig, 1.0),
+                                                                      0.0))),
+                      "reference": [float(x) for x in r], "gpu": [float(x) for x in g],
+                      "rel_diff": [float(x) for x in rel], "sigma_chaos": [float(x) for x in sig]},
+            "dv_model": {"within_tolerance": int(ok_a.sum()),
+                         "max_d_over_sigma_chaos": float(np.max(np.where(sig_a > 0, np.abs(Ag - A) /
+                                                                         np.where(sig_a > 0, sig_a, 1.0), 0.0))),
+                         "reference": [float(x) for x in A], "gpu": [float(x) for x in Ag],
+                         "rel_diff": [float(x) for x in rel_a], "sigma_chaos": [float(x) for x in sig_a]},
+            "diverged_walks": [int(x) for x in nd.sum(1)]}
+
+
 def compare_to_reference(gpu: ApparentResistivity, ref: ReferenceSurvey, replicas: np.ndarray | None = None) -> dict:
     """The north-star check (BASELINE.json): RMSE of rho_a(GPU) - rho_a(reference) over
     the dipoles the reference resolves, against the reference's 1-sigma Monte-Carlo
@@ -394,6 +546,10 @@ class WennerSurveyResult:
     launches: int             # multi-source solves (per field)
     kernel_ms: float          # walk-kernel time, both fields (this rank)
     local_walk_steps: int = 0  # this rank's walk-steps (= walk_steps on one GPU)
+    # with a communicator, this rank's wall-clock ms summed over the groups' protocols:
+    # wait_ms (the collective thread waiting for the local solves' results), agree_ms (the
+    # agreement all-reduce: waits for the slowest rank), gather_ms, merge_ms
+    phase_ms: dict | None = None
 
 
 def wenner_batches(n_electrodes: int, a: int = 1, max_sources: int = 16):
@@ -417,7 +573,8 @@ def group_seed(seed: int, g: int) -> int:
     return (int(seed) * 0x9E3779B1 + g) & (2**64 - 1)
 
 
-def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent=True):
+def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent=True,
+                            phase_ms: dict | None = None):
     """The model and background fields of a multi-source survey across the ranks of one
     communicator. Worker threads (one per field and handle pair, or one per handle pair
     without ``concurrent``) solve this rank's walk range of every group
@@ -472,7 +629,10 @@ def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, rec
         for g, (j0, j1, t0, t1) in enumerate(batches):
             S = t1 - t0
             for f in (0, 1):
+                t_wait = time.perf_counter()
                 blocks, err, tm = slots[f][g].get()
+                if phase_ms is not None:
+                    phase_ms["wait_ms"] = phase_ms.get("wait_ms", 0.0) + 1e3 * (time.perf_counter() - t_wait)
 
                 def solve_range(a, b, blocks=blocks, err=err):
                     if err is not None:
@@ -482,8 +642,12 @@ def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, rec
                     return blocks
 
                 key = solve_key(group_seed(seed, g), sc.eps, sc.max_steps, sc.points[j0:j1])
+                ph = {}
                 sums, _, all_steps = run_protocol(R, rank, j1 - j0, int(n_walks), 2 * S + 1, solve_range,
-                                                  comm.allreduce, comm.allgather, key=key)
+                                                  comm.allreduce, comm.allgather, key=key, phases=ph)
+                if phase_ms is not None:
+                    for name in ("agree_ms", "gather_ms", "merge_ms"):
+                        phase_ms[name] = phase_ms.get(name, 0.0) + ph[name]
                 stats = _stats_of_multi(sums, int(n_walks))
                 st = SolveStats(mean=np.stack([x.mean for x in stats]), stderr=np.stack([x.stderr for x in stats]),
                                 mean_steps=stats[0].mean_steps, walks=int(n_walks), total_steps=int(all_steps),
@@ -561,8 +725,10 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
                                     eps=sc.eps, seed=group_seed(seed, g), return_stats=True)
             record(f, g, st, st.total_steps)
 
+    phase_ms = None
     if comm is not None:
-        _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent)
+        phase_ms = {"wait_ms": 0.0, "agree_ms": 0.0, "gather_ms": 0.0, "merge_ms": 0.0}
+        _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent, phase_ms)
     elif concurrent:
         from concurrent.futures import ThreadPoolExecutor
 
@@ -579,4 +745,4 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
     dm = DipoleData(mean[0][q, M] - mean[0][q, N], np.sqrt(se[0][q, M] ** 2 + se[0][q, N] ** 2))
     dh = DipoleData(mean[1][q, M] - mean[1][q, N], np.sqrt(se[1][q, M] ** 2 + se[1][q, N] ** 2))
     return WennerSurveyResult(quad, dm, dh, apparent_resistivity(dm, dh, 1.0 / alpha_bg), steps, launches, kms,
-                              acc[0][2] + acc[1][2])
+                              acc[0][2] + acc[1][2], phase_ms)

@@ -292,6 +292,10 @@ typedef struct {
     wost_timing local;          /* this rank's solve (walk kernel time, steps) */
     int64_t walk_begin, walk_end;   /* this rank's walk range of every point */
     uint64_t total_steps;       /* walk-steps of all ranks */
+    /* wall-clock phases of the protocol on this rank (wost_dist_last_phases): the local
+     * solve and pack, the agreement all-reduce (it waits for the slowest rank's local
+     * solve), the block all-gather and the ordered merge */
+    double local_ms, agree_ms, gather_ms, merge_ms;
 } wost_dist_timing;
 
 int wost_comm_unique_id(uint8_t* id);
@@ -372,6 +376,11 @@ int wost_dist_solve_key(uint64_t seed, float eps, int32_t max_steps, const float
 int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank, int64_t n_points,
                          int64_t walks_per_point, int32_t row, double* point_stats,
                          int64_t* walk_begin, int64_t* walk_end, uint64_t* total_steps);
+/* The calling thread's last wost_distributed_run, in wall-clock ms: ms[0] the local
+ * solve and pack, ms[1] the agreement all-reduce, ms[2] the block all-gather, ms[3] the
+ * merge (a phase not reached is 0). Per thread, so concurrent protocols on other threads
+ * do not overwrite it. */
+int wost_dist_last_phases(double* ms);
 
 /* Walk kernels: by default libwost compiles a field-specialised walk kernel per
  * handle and kernel variant with hiprtc (cached in memory and in
@@ -379,6 +388,22 @@ int wost_distributed_run(const wost_dist_ops* ops, int32_t n_ranks, int32_t rank
  * interpreting kernel if that fails. enable = 0 forces the precompiled kernel
  * (also: environment WOST_JIT=0). Both give identical results. */
 int wost_set_jit(wost_handle* h, int32_t enable);
+
+/* The walk direction's cos and sin (solvers/WoStSolver.py:230-232). The reference's
+ * torch.cos/torch.sin return the exact values rounded to float32 within their own ulp;
+ * on a walk that hits a curved Neumann boundary a one-ulp change of a direction sends it
+ * elsewhere (C5: ~20% of the walks), so:
+ *   WOST_TRIG_EXACT  correctly rounded, evaluated in double precision (C5: 93% of the
+ *                    reference's replayed walks identical, as the oracle; 3% slower there,
+ *                    13-24% on the short-step scenarios);
+ *   WOST_TRIG_FAST   the hardware's v_sin/v_cos (a few ulps; C5: 83% identical);
+ *   WOST_TRIG_AUTO   (default) exact when the Neumann polyline has >= 3 segments (a
+ *                    curved boundary: C3's circle, C5's topography), fast otherwise
+ *                    (Dirichlet-only problems and the DCR scenarios' straight top, whose
+ *                    walks match the reference's either way).
+ * Environment: WOST_TRIG = auto | exact | fast (the default of new handles). */
+enum wost_trig { WOST_TRIG_AUTO = 0, WOST_TRIG_EXACT = 1, WOST_TRIG_FAST = 2 };
+int wost_set_trig(wost_handle* h, int32_t mode);
 
 /* compat="fixed" with delta tracking: the corrected screened law moves a walk
  * ~2/sqrt(sigma_bar) per collision, so a point at Dirichlet distance d needs

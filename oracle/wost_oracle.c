@@ -544,7 +544,9 @@ static void orc_walk(const orc_ctx* c, uint64_t wid, float x0, float y0, float* 
         orc_philox(ctr, c->k0, c->k1, rn);
         float theta = (orc_u01(rn[0]) * 2.0f) * (float)ORC_PI;      /* :226 */
         if (onB && c->neu) theta = theta / 2.0f + atan2f(ny, nx);    /* :227-228 */
-        float cs = cosf(theta), sn = sinf(theta);                    /* :230-232 */
+        /* :230-232, the exact values rounded to float32 (torch's MKL cos/sin within
+           its own ulp; the device's sincos_rn gives the same bits, tests/test_trig_rn.py) */
+        float cs = (float)cos((double)theta), sn = (float)sin((double)theta);
         if (orc_dir_perturb != 0.0f) { cs *= 1.0f + orc_dir_perturb; sn *= 1.0f - orc_dir_perturb; }
         float xnx, xny;
         if (c->neu) {                                                /* :236 */

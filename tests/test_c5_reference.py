@@ -167,3 +167,60 @@ def test_oracle_replays_reference_c5_walks():
     m_o = v.astype(np.float64).reshape(n, -1).mean(1)
     m_r = z["walk_values"].reshape(n, -1).mean(1)
     np.testing.assert_allclose(m_o, m_r, rtol=1e-3, atol=1e-6 * np.abs(m_r).max())
+
+
+# ---------------------------------------------------------------- C5 apparent resistivity (G13)
+def oracle_wenner_walks(ref, sc):
+    """survey.wenner_replay_walks' solver on the oracle: only the receivers' walk ranges."""
+    from dcrmontecarlo_amd import fields as F
+
+    def solve_walks(f, pts, srcs, W, seed, rows):
+        vals = np.zeros((len(srcs), len(pts), W), np.float32)
+        steps = np.zeros((len(pts), W), np.uint32)
+        alpha = sc.alpha if f == 0 else F.const(ref.alpha_bg)
+        for j, src in enumerate(srcs):
+            pb = O.Problem(sc.dirichlet, sc.neumann, sc.g, src, sc.sigma, alpha, sigma_bar=ref.sigma_bar)
+            for e in rows:
+                v, st = pb.solve_walks(pts, W, sc.max_steps, sc.eps, seed, wid_begin=e * W, wid_end=(e + 1) * W)
+                vals[j, e], steps[e] = v, st
+        return vals, steps
+
+    return solve_walks
+
+
+def test_c5_rho_replay_fixture_is_the_survey_layout():
+    """G13 (rho_replay_wenner_topography_physical.npz): the receivers are the quadripoles'
+    M and N, their groups and seeds those of survey.run_wenner_survey, model and
+    background walks share their paths (common random numbers)."""
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd import survey as SV
+
+    z = golden("rho_replay_wenner_topography_physical.npz")
+    ref = SV.load_wenner_replay(os.path.join(HERE, "golden", "rho_replay_wenner_topography_physical.npz"))
+    sc = S.wenner_topography_physical(n_walks=1)
+    np.testing.assert_array_equal(ref.points, sc.points)
+    np.testing.assert_array_equal(ref.receivers, ref.quadripoles[:, 1:3])
+    batches = list(SV.wenner_batches(len(sc.points)))
+    for i in range(len(ref.quadripoles)):
+        for k in range(2):
+            g = int(ref.groups[i, k])
+            j0, j1, t0, t1 = batches[g]
+            assert j0 <= ref.receivers[i, k] < j1 and t0 <= ref.quadripoles[i, 0] < t1
+            assert int(z["group_seeds"][i, k]) == SV.group_seed(ref.survey_seed, g)
+    assert bool(z["common_paths"]) and np.array_equal(ref.model_steps, ref.background_steps)
+    assert ref.sigma_bar == pytest.approx(float(golden("fields_wenner_topography_physical.npz")["sigma_bar"]), rel=1e-12)
+
+
+def test_oracle_replays_reference_c5_rho_a():
+    """The oracle on the reference's C5 Wenner walks (4 of the 16 quadripoles): >= 96% of
+    the walks identical, and every quadripole's dV and rho_a within the bound the
+    diverged walks allow (survey.compare_wenner_replay)."""
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd import survey as SV
+
+    ref = SV.load_wenner_replay(os.path.join(HERE, "golden", "rho_replay_wenner_topography_physical.npz"))
+    ref = SV.wenner_replay_subset(ref, [1, 6, 9, 13])
+    sc = S.wenner_topography_physical(n_walks=1)
+    out = SV.compare_wenner_replay(*SV.wenner_replay_walks(ref, oracle_wenner_walks(ref, sc)), ref)
+    assert out["walks_identical"] >= 0.96, out["walks_identical"]
+    assert out["all_within_tolerance"], out

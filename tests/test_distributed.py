@@ -201,7 +201,17 @@ def _store_worker(rank, world, port, mode, out_q):
             store.close()
 
 
-@pytest.mark.parametrize("mode", ["socket", "agent_file", "agent_tcp"])
+def _nested_store_worker(rank, world, port, out_q):
+    """A rank below a wrapper process of its own (`--no-python` scripts, env
+    wrappers): the ranks no longer share a parent."""
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_store_worker, args=(rank, world, port, "agent_file", out_q))
+    p.start()
+    p.join(timeout=120)
+    raise SystemExit(p.exitcode)
+
+
+@pytest.mark.parametrize("mode", ["socket", "agent_file", "agent_file_nested", "agent_tcp"])
 def test_communicator_id_travels_through_the_launch_store(mode):
     """Communicator.from_env's id exchange (the part that needs no GPU): rank 0's 128 bytes
     reach every rank -- rank 0 hosting the standard-library socket store (bench.py's own
@@ -215,7 +225,10 @@ def test_communicator_id_travels_through_the_launch_store(mode):
                          wait_for_workers=False) if mode == "agent_tcp" else None
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_store_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    if mode == "agent_file_nested":
+        procs = [ctx.Process(target=_nested_store_worker, args=(r, world, port, q)) for r in range(world)]
+    else:
+        procs = [ctx.Process(target=_store_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
@@ -223,7 +236,8 @@ def test_communicator_id_travels_through_the_launch_store(mode):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(res[r][0] == bytes(range(128)) for r in range(world))
-    want = {"socket": "SocketStore", "agent_file": "_FileStore", "agent_tcp": "TCPStore"}[mode]
+    want = {"socket": "SocketStore", "agent_file": "_FileStore", "agent_file_nested": "_FileStore",
+            "agent_tcp": "TCPStore"}[mode]
     assert all(res[r][2] == want for r in range(world)), res
     if mode != "agent_tcp":
         assert not any(res[r][1] for r in range(world)), "torch was imported"
@@ -292,6 +306,8 @@ def _protocol_worker(rank, world, port, W, mode, out_q):
     myW = W + 4096 if (mode == "disagree" and rank == 1) else W
     seed = 100 if (mode == "disagree_seed" and rank == 1) else 99
     key = D.solve_key(seed, sc.eps, sc.max_steps, pts) if mode.startswith("disagree_") or mode == "ok" else None
+    if mode == "nan_eps":   # every rank passes the same NaN: still no agreement
+        key = D.solve_key(seed, float("nan"), sc.max_steps, pts)
 
     def solve_range(w0, w1):
         if mode == "fail" and rank == world - 1:
@@ -364,6 +380,14 @@ def test_library_protocol_rejects_disagreeing_ranks(mode):
         assert "arguments" in res[0][1]
 
 
+def test_library_protocol_refuses_a_nan_argument_on_every_rank():
+    """A NaN in the agreement key (here eps, the same NaN on every rank) cannot be agreed
+    on: each rank fails it locally and every rank returns ValueError."""
+    res = _run_protocol_world(2, 2 * 4096, "nan_eps")
+    for r in range(2):
+        assert res[r][0] == "ValueError" and "NaN" in res[r][1], res[r]
+
+
 def test_solve_key_covers_seed_eps_steps_and_points():
     from dcrmontecarlo_amd import scenarios as S
 
@@ -397,3 +421,28 @@ def test_library_protocol_eight_thread_ranks_with_oracle_shards():
     assert sum(1 for r in range(R) if res[r][1][0] == res[r][1][1]) == 2
     for r in range(R):
         assert np.array_equal(res[r][0], single)
+
+
+def test_socket_store_is_set_once_bounded_and_local():
+    """the store listens on MASTER_ADDR only, refuses a second set of a key
+    (no peer can replace rank 0's id) and drops a request whose length prefix exceeds its
+    cap instead of allocating it."""
+    import socket
+    import struct
+
+    from dcrmontecarlo_amd import comm
+
+    port = _free_port()
+    st = comm.SocketStore("127.0.0.1", port, is_master=True, timeout=10)
+    try:
+        assert st._srv.server_address[0] == "127.0.0.1"
+        st.set("id", b"abc")
+        with pytest.raises(KeyError):
+            st.set("id", b"evil")
+        assert st.get("id") == b"abc"
+        with socket.create_connection(("127.0.0.1", port), timeout=10) as c:
+            c.sendall(b"S" + struct.pack(">I", 3) + b"big" + struct.pack(">I", 1 << 31))
+            assert c.recv(1) == b""          # the server closed the connection
+        assert st.get("id") == b"abc"
+    finally:
+        st.close()

@@ -7,10 +7,11 @@ tests/test_c5_reference.py for the fixtures and the tolerances' origin):
   reference's silhouette distances and intersections at 320 recorded C5 walk positions,
   and the device's full scans bit for bit;
 * the reference's C5 walks replayed on the Philox stream (8 electrodes x 32 walks):
-  the device's walks (tree kernel, field-specialised) agree at least as often as the
-  oracle agrees with itself under a 1-ulp change of the step direction, less 2 points,
-  >= 95% of the walk values are within 1e-4, and the per-electrode means agree within
-  3 combined standard errors.
+  the device's walks (tree kernel, field-specialised) are the oracle's and agree with
+  the reference's as often as the oracle's do (less 0.02), >= 95% of the walk values
+  are within 1e-4, and the per-electrode means agree within 1e-3;
+* G13: the reference's C5 Wenner survey (physical fields) replayed on the same walks:
+  every quadripole's dV and rho_a within the bound its diverged walks allow.
 """
 import numpy as np
 import pytest
@@ -68,6 +69,15 @@ def test_c5_device_tree_queries_refuse_other_ops(gpu_available):
 
 
 def test_c5_device_replays_reference_walks(gpu_available):
+    """The reference's C5 walks on the Philox stream, the device's tree kernel with its
+    own sigma_bar and the default trig (wost_set_trig AUTO: correctly rounded directions
+    on this curved boundary; the segment angles from the C library's atan2f, as torch's).
+    Round 4's device left the reference's path at the first step of every walk (hardware
+    v_sin/v_cos, the device's atan2f on half of the segments: tools/r05/c5_divergence.py)
+    and kept 82% of the walks; now its walks are the oracle's (>= 99% identical) and it
+    keeps as many of the reference's as the oracle does (0.930, the remaining 7% the
+    reference's own MKL cos/sin ulps and 10k-element torch reductions). Per-electrode
+    means within 1e-3 as the oracle's (tests/test_c5_reference.py)."""
     from oracle import oracle as O
 
     from dcrmontecarlo_amd import scenarios as S
@@ -83,25 +93,45 @@ def test_c5_device_replays_reference_walks(gpu_available):
     v, st = s.solve_walks(z["points"], nWalks=W, maxSteps=int(z["max_steps"]), eps=float(z["eps"]),
                           seed=int(z["seed"]))
     assert s.last_timing["tree"] == 1
-    same, close = c5_replay_agreement(v.ravel(), st.ravel(), z)
-    # the oracle's own 1-ulp chaos on the same walks (its own sigma_bar)
+    v, st = v.ravel(), st.ravel()
+    same, close = c5_replay_agreement(v, st, z)
     pb = O.Problem(z["dirichlet"], z["neumann"], sc.g, sc.f, sc.sigma, sc.alpha)
     pb = O.Problem(z["dirichlet"], z["neumann"], sc.g, sc.f, sc.sigma, sc.alpha, sigma_bar=pb.sigma_bar())
-    args = (z["points"], W, int(z["max_steps"]), float(z["eps"]), int(z["seed"]))
-    ov, os_ = pb.solve_walks(*args)
-    try:
-        O.set_direction_perturbation(1.2e-7)
-        pv, ps = pb.solve_walks(*args)
-    finally:
-        O.set_direction_perturbation(0.0)
+    ov, os_ = pb.solve_walks(z["points"], W, int(z["max_steps"]), float(z["eps"]), int(z["seed"]))
+    o_same, _ = c5_replay_agreement(ov, os_, z)
     scale = max(float(np.abs(ov).max()), 1e-30)
-    chaos = float(((ps == os_) & (np.abs(pv - ov) <= 1e-3 * np.abs(ov) + 1e-5 * scale)).mean())
-    assert same >= chaos - 0.02, (same, chaos)
+    dev_oracle = float(((st == os_) & (np.abs(v - ov) <= 1e-3 * np.abs(ov) + 1e-5 * scale)).mean())
+    print(f"C5 replay: device walks identical to the reference's {same:.4f} (oracle {o_same:.4f}), "
+          f"to the oracle's {dev_oracle:.4f}")
+    assert dev_oracle >= 0.99, dev_oracle
+    assert same >= o_same - 0.02 and same >= 0.906 - 0.02, (same, o_same)
     assert close >= 0.95, close
-    # per-electrode means within 3 combined standard errors: a walk that diverged (chaos)
-    # carries a heavy-tailed value of the literal fields, so exact means are not expected
     n = len(z["points"])
-    g = v.astype(np.float64).reshape(n, -1)
-    r = z["walk_values"].reshape(n, -1)
-    se = np.sqrt(g.var(1, ddof=1) / W + r.var(1, ddof=1) / W)
-    assert np.all(np.abs(g.mean(1) - r.mean(1)) <= 3.0 * se + 1e-9 * np.abs(r).max()), (g.mean(1), r.mean(1), se)
+    m_g = v.astype(np.float64).reshape(n, -1).mean(1)
+    m_r = z["walk_values"].reshape(n, -1).mean(1)
+    np.testing.assert_allclose(m_g, m_r, rtol=1e-3, atol=1e-6 * np.abs(m_r).max())
+
+
+def test_c5_device_replays_reference_rho_a(gpu_available):
+    """G13: the reference's own C5 Wenner survey (setSourceTerm + _solveUnified on the
+    Philox stream, physical conductivity and background, 16 quadripoles x both receivers x
+    64 walks; tests/golden/rho_replay_wenner_topography_physical.npz) against the device on
+    the same walks, launched per electrode group as run_wenner_survey launches them: the
+    walks identical at least as often as the oracle's (0.980 on all 16 quadripoles) less
+    0.02, and every quadripole's dV and rho_a within the bound its diverged walks allow
+    (survey.compare_wenner_replay)."""
+    import os
+
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd import survey as SV
+
+    ref = SV.load_wenner_replay(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                             "rho_replay_wenner_topography_physical.npz"))
+    sc = S.wenner_topography_physical(n_walks=1)
+    sm = sc.solver(device=0)
+    sh = SV.homogeneous_solver(sc, ref.alpha_bg, sm, device=0)
+    out = SV.compare_wenner_replay(*SV.wenner_replay_walks(ref, SV.solver_replay_walks(sm, sh, ref)), ref)
+    print("C5 rho_a replay: walks identical", out["walks_identical"], "diverged per quadripole",
+          out["diverged_walks"], "dV max d/sigma_chaos", out["dv_model"]["max_d_over_sigma_chaos"])
+    assert out["walks_identical"] >= 0.96, out["walks_identical"]
+    assert out["all_within_tolerance"], out

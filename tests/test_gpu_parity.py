@@ -269,14 +269,16 @@ def test_device_matches_oracle(gpu_available, name):
 
 # ---------------------------------------------------------------- statistics vs the reference's own RNG
 STAT_WALKS = {"laplace_square": 20000, "manufactured_polynomial": 20000, "poisson_square": 20000,
-              "variable_coefficients": 20000, "dcr_dipole": 20000, "notebook_dcr": 4000}
+              "variable_coefficients": 20000, "dcr_dipole": 20000, "notebook_dcr": 4000,
+              "wenner_topography": 20000, "wenner_topography_physical": 20000}
 
 
-@pytest.mark.parametrize("name", SCEN)
+@pytest.mark.parametrize("name", SCEN + ["wenner_topography", "wenner_topography_physical"])
 def test_statistics_vs_reference_rng(gpu_available, name):
     """Against the reference run with its OWN random streams (torch/numpy RNG): every
     reference per-point mean (n walks) is a plausible n-walk mean of the device's walks
-    (bootstrap, two-sided p > 1e-3 per point); likewise the mean walk lengths."""
+    (bootstrap, two-sided p > 1e-3 per point); likewise the mean walk lengths. C5 (round
+    5): 16 electrodes x 200 reference walks on the 10k-segment topography, both fields."""
     from test_oracle_golden import bootstrap_pvalues
 
     z = golden(f"stats_{name}.npz")

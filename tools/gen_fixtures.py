@@ -404,12 +404,16 @@ def gen_sampler_draws(n=20000):
 _NODES = {}
 
 
-def replay(name, points, n_walks, max_steps, eps, seed, wid0=0, spec=None, values_only=False):
+def replay(name, points, n_walks, max_steps, eps, seed, wid0=0, spec=None, values_only=False, sigma_bar=None):
     """The reference's solve() on the Philox stream. Walk ids start at wid0 and count
     up per walk (point-major), so a job holding walks [c0, c0+n) of point e of a
-    W-walk solve passes wid0 = e*W + c0 and replays exactly those walks."""
+    W-walk solve passes wid0 = e*W + c0 and replays exactly those walks. ``sigma_bar``
+    replaces the solver's own (a homogeneous background solved with the model's, as
+    survey.homogeneous_solver does: common random numbers)."""
     spec = spec if spec is not None else ref_scenarios()[name]()
     solver = build_ref_solver(spec)
+    if sigma_bar is not None:
+        solver.sigma_bar = float(sigma_bar)
     k0, k1 = seed & M32, (seed >> 32) & M32
     st = {"wid": wid0, "step": -1, "nrand": 0}
     cache = {}
@@ -541,6 +545,10 @@ def gen_replays(names):
 # G6: statistics with the reference's own RNG
 # ---------------------------------------------------------------------------
 STATS = {
+    # C5: 16 electrodes along the line, 200 walks each (the reference scans all 10k
+    # segments twice per step: ~1.6 ms per step, ~1 min per electrode)
+    "wenner_topography": lambda: (S.wenner_topography(n_walks=1).points[8::16], 200, 500, 0.9),
+    "wenner_topography_physical": lambda: (S.wenner_topography_physical(n_walks=1).points[8::16], 200, 500, 0.9),
     "laplace_square": lambda: (S.laplace_square().points[:32], 500, 1000, 1e-4),
     "manufactured_polynomial": lambda: (S.manufactured_polynomial().points, 150, 800, 1e-4),
     "poisson_square": lambda: (S.poisson_square().points[:16], 400, 500, 1e-4),
@@ -710,6 +718,101 @@ def gen_rho_replay(walks, workers, chunk=100):
     print("rho_replay_dcr_dipole.npz", f"{time.time() - t0:.0f}s", "common paths", same, "sigma_bar", sbar)
 
 
+# ---------------------------------------------------------------------------
+# G13: the C5 Wenner survey's apparent resistivity replayed on the Philox stream --
+# the reference's setSourceTerm(transmitter) + _solveUnified (WoStSolver.py:150-157,
+# 162-316) at both receivers of 16 quadripoles, for the physical conductivity and the
+# homogeneous background (alpha = 0.01, the model's sigma_bar: common random numbers),
+# each receiver's walks carrying the ids and the seed they have in the device's survey
+# (survey.run_wenner_survey: electrode groups of 15, group_seed), so that rho_a is
+# pinned walk for walk
+# ---------------------------------------------------------------------------
+C5_RHO_SEED = 505
+C5_ALPHA_BG = 1e-2          # notebook cell 17's background_conductivity (rho_bg = 100)
+C5_WIDTH = 0.5              # survey.dipole_source's electrode width
+
+
+def tx_source(a, b, width=C5_WIDTH):
+    """A Wenner transmitter as the reference writes a current source (notebook cell 17's
+    dcr_current_source_torch, with +1 A at electrode a and -1 A at electrode b)."""
+    ax, ay, bx, by = (float(v) for v in (a[0], a[1], b[0], b[1]))
+
+    def f(point):
+        x, y = point[0], point[1]
+        norm = 1.0 / (2 * torch.pi * width**2)
+        positive_source = norm * torch.exp(-((x - ax) ** 2 + (y - ay) ** 2) / (2 * width**2))
+        negative_sink = -norm * torch.exp(-((x - bx) ** 2 + (y - by) ** 2) / (2 * width**2))
+        return float(positive_source + negative_sink)
+
+    return f
+
+
+def _c5_rho_worker(args):
+    field, q, k, e, W, seed_g, wid0, sigma_bar = args
+    torch.set_num_threads(1)
+    from dcrmontecarlo_amd import survey as SV  # noqa: F401 (the device survey's grouping, documented)
+
+    sc = S.wenner_topography_physical(n_walks=1)
+    spec = ref_scenarios()["wenner_topography_physical"]()
+    spec["f"] = tx_source(sc.points[q], sc.points[q + 3])
+    if field == "background":
+        spec["alpha"] = lambda p: C5_ALPHA_BG + 0.0 * p[0]
+    pt = np.ascontiguousarray(sc.points[e:e + 1], np.float32)
+    v, s, sb = replay("wenner_topography_physical", pt, W, sc.max_steps, sc.eps, seed_g, wid0=wid0, spec=spec,
+                      values_only=True, sigma_bar=sigma_bar)
+    return field, q, k, v, s, sb
+
+
+def gen_c5_rho_replay(walks, workers, n_quads=16):
+    import multiprocessing as mp
+
+    from dcrmontecarlo_amd import survey as SV
+
+    sc = S.wenner_topography_physical(n_walks=1)
+    E = len(sc.points)
+    quad = SV.wenner_quadripoles(E)
+    qsel = np.unique(np.linspace(0, len(quad) - 1, n_quads).round().astype(np.int64))
+    batches = list(SV.wenner_batches(E))
+    group_of = {}
+    for g, (j0, j1, t0, t1) in enumerate(batches):
+        for j in range(j0, j1):
+            group_of[j] = (g, j0)
+    spec = ref_scenarios()["wenner_topography_physical"]()
+    with _quiet():
+        sigma_bar = float(build_ref_solver(spec).sigma_bar)
+    _NODES[sigma_bar] = screened_nodes(sigma_bar)     # forked workers inherit the sampler table
+    jobs, meta = [], np.zeros((len(qsel), 2, 4), np.int64)   # per (quad, receiver): electrode, group, j0, seed_g
+    for i, q in enumerate(qsel):
+        for k, e in enumerate((quad[q, 1], quad[q, 2])):       # receivers M, N
+            g, j0 = group_of[int(e)]
+            seed_g = SV.group_seed(C5_RHO_SEED, g)
+            meta[i, k] = (e, g, j0, seed_g if seed_g < 2**63 else seed_g - 2**64)
+            for field in ("model", "background"):
+                jobs.append((field, int(q), k, int(e), walks, seed_g, (int(e) - j0) * walks, sigma_bar))
+    vals = {f: np.zeros((len(qsel), 2, walks)) for f in ("model", "background")}
+    steps = {f: np.zeros((len(qsel), 2, walks), np.int32) for f in ("model", "background")}
+    row = {int(q): i for i, q in enumerate(qsel)}
+    t0 = time.time()
+    with mp.get_context("fork").Pool(workers) as pool:
+        for n, (field, q, k, v, s, sb) in enumerate(pool.imap_unordered(_c5_rho_worker, jobs)):
+            vals[field][row[q], k] = v
+            steps[field][row[q], k] = s
+            assert sb == sigma_bar, (sb, sigma_bar)
+            if n % 8 == 7:
+                print(f"c5_rho_replay: {n + 1}/{len(jobs)} jobs, {time.time() - t0:.0f}s", flush=True)
+    same = bool(np.array_equal(steps["model"], steps["background"]))
+    np.savez_compressed(os.path.join(OUT, "rho_replay_wenner_topography_physical.npz"), points=sc.points,
+                        quadripoles=quad[qsel], quad_index=qsel, receivers=meta[:, :, 0], groups=meta[:, :, 1],
+                        group_j0=meta[:, :, 2], group_seeds=meta[:, :, 3].astype(np.int64).view(np.uint64),
+                        survey_seed=np.uint64(C5_RHO_SEED), n_walks=np.int64(walks), max_steps=np.int64(sc.max_steps),
+                        eps=np.float32(sc.eps), alpha_bg=np.float64(C5_ALPHA_BG), width=np.float64(C5_WIDTH),
+                        sigma_bar=np.float64(sigma_bar), model_values=vals["model"],
+                        background_values=vals["background"], model_steps=steps["model"],
+                        background_steps=steps["background"], common_paths=np.bool_(same))
+    print("rho_replay_wenner_topography_physical.npz", f"{time.time() - t0:.0f}s", "common paths", same,
+          "sigma_bar", sigma_bar, "mean steps", float(steps["model"].mean()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="geometry,fields,greens,sampler,replay,stats")
@@ -717,6 +820,7 @@ def main():
     ap.add_argument("--stats-workers", type=int, default=8)
     ap.add_argument("--rho-walks", type=int, default=400)
     ap.add_argument("--rho-replay-walks", type=int, default=256)
+    ap.add_argument("--c5-rho-walks", type=int, default=64)
     a = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     parts = set(a.only.split(","))
@@ -742,6 +846,8 @@ def main():
         gen_rho(a.rho_walks, a.stats_workers)
     if "rho_replay" in parts:
         gen_rho_replay(a.rho_replay_walks, a.stats_workers)
+    if "c5_rho_replay" in parts:
+        gen_c5_rho_replay(a.c5_rho_walks, a.stats_workers)
 
 
 if __name__ == "__main__":
