@@ -50,7 +50,7 @@ namespace {
 // Each bit only selects one fixed code path.
 int exp_flags() {
     const char* e = std::getenv("WOST_EXP_FLAGS");
-    return e ? (int)std::strtol(e, nullptr, 10) & 0xFFFFF : 0;
+    return e ? (int)std::strtol(e, nullptr, 10) & 0x3FFFFFFF : 0;
 }
 
 // the squared segment length exactly as the kernel forms it
@@ -403,6 +403,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 65536) o << "#define WOST_ABL_NO_SILHOUETTE 1\n";
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
+    if (exp_flags() >> 18) o << "#define WOST_ABL_DUP " << (exp_flags() >> 18) << "\n";   // phase_dup.sh
     o << "#define WOST_JIT_TRIG_EXACT " << (exact_trig ? 1 : 0) << "\n";   // wost_set_trig
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
     if (const char* e = std::getenv("WOST_JIT_PHILOX_AHEAD"))   // A/B: Philox one step ahead

@@ -717,6 +717,38 @@ __device__ __forceinline__ void pool_unlock(uint32_t* pool, int lane, uint32_t n
     if (lane == 0) __hip_atomic_store(pool, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Phase markers of the walk step for the offline ISA budget (tools/r05/phase_isa.py,
+// WOST_PHASE_MARKS builds only): an assembly comment, which also bounds the instruction
+// scheduler's regions, so the marked kernel is a study build, never the one that runs.
+#if defined(WOST_PHASE_MARKS)
+#define WOST_PHASE(name) asm volatile("; @phase " name)
+#else
+#define WOST_PHASE(name)
+#endif
+
+// Study builds (tools/r05/phase_dup.sh; WOST_EXP_FLAGS bits 2^18 and up, A/B only): a
+// phase of the walk step computed a second time from opaque copies of its inputs and
+// merged so that it cannot be removed yet changes no bit (x | (y & opaque 0)), so the
+// walks are the same walks and the dynamic VALU counter grows by that phase's cost plus
+// the merge's ~3 instructions. 1 Dirichlet distance, 2 Philox draw, 4 direction cos/sin,
+// 8 Neumann ray query (scan kernels), 16 radial sampler, 32 screened G_norm, 64 alpha jet
+// at the sample, 128 alpha at the ray's point, 256 the source f, 512 sigma'.
+#ifndef WOST_ABL_DUP
+#define WOST_ABL_DUP 0
+#endif
+__device__ __forceinline__ float dup_opq(float v) {
+    __asm__ volatile("" : "+v"(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t dup_zero() {
+    uint32_t z = 0u;
+    __asm__ volatile("" : "+v"(z));
+    return z;
+}
+__device__ __forceinline__ float dup_merge(float a, float b) {   // a, depending on b
+    return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, a) | (__builtin_bit_cast(uint32_t, b) & dup_zero()));
+}
+
 // The direction's cos and sin (wost_set_trig): correctly rounded (sincos_rn, the
 // reference's values but for its own ulp errors; double-precision arithmetic) or the
 // hardware's v_sin/v_cos (a few ulps, tens near the zeros). The field-specialised kernels
@@ -1054,7 +1086,9 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #if defined(WOST_TREE_ITER_STATS)
         ic_arr[14] += 1u;
 #endif
-        const float dd = fld.dirichlet_distance(dP, A.nd, px, py);  // :208
+        WOST_PHASE("dirichlet_distance");
+        float dd = fld.dirichlet_distance(dP, A.nd, px, py);        // :208
+        if (WOST_ABL_DUP & 1) dd = dup_merge(dd, fld.dirichlet_distance(dP, A.nd, dup_opq(px), py));
         if (FIX && stepping && !(dd > A.eps)) {   // Q7/Q12 fixed: stop here, g at this point
             dD = dd;
             if (!kWaveTree) continue;
@@ -1080,6 +1114,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 WOST_OPAQUE_SGPR(key0);
                 WOST_OPAQUE_SGPR(key1);
                 rn = philox_draw(pw, (uint32_t)k, key0, key1);       // philox4x32_10({k, 0, wid})
+                if (WOST_ABL_DUP & 2) {
+                    const U4 r2 = philox_draw(pw, (uint32_t)k | dup_zero(), key0, key1);
+                    rn.x |= (r2.x ^ r2.y ^ r2.z ^ r2.w) & dup_zero();
+                }
             }
 #endif
             float theta = (u01(rn.x) * 2.0f) * kPiF;                 // :226
@@ -1089,9 +1127,16 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             onB0 = onB;
             phi0 = phi;
             walk_sincos(theta, sn, cs, A.exact_trig != 0);           // :230-232
+            if (WOST_ABL_DUP & 4) {
+                float s2, c2;
+                walk_sincos(dup_opq(theta), s2, c2, A.exact_trig != 0);
+                sn = dup_merge(sn, s2);
+                cs = dup_merge(cs, c2);
+            }
         };
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
+        WOST_PHASE("silhouette");
         if (NEU) {
 #if defined(WOST_ABL_NO_SILHOUETTE)   // ablation (timing only)
             const float dn = WOST_INF;
@@ -1107,6 +1152,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         } else {
             r = dd > A.rmin ? dd : A.rmin;                           // :215
         }
+        WOST_PHASE("philox_direction");
         draw_direction();
 #if !defined(WOST_ABL_NO_PHILOX)
         if (WOST_PHILOX_AHEAD) {   // the next step's words, overlapping this step's arithmetic
@@ -1119,14 +1165,22 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #endif
 
         float xnx, xny;
+        WOST_PHASE("ray_query");
         if (NEU) {                                                   // :235-236
 #if defined(WOST_ABL_NO_RAY)
             Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
 #else
-            const Hit h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws,
-                                                                                lane, WOST_IC)
-                          : FIX       ? fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r)
-                                      : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
+            Hit h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws,
+                                                                          lane, WOST_IC)
+                    : FIX       ? fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r)
+                                : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
+            if ((WOST_ABL_DUP & 8) && !kWaveTree && !FIX) {
+                const Hit h2 = fld.neumann_intersect(nP, A.nn, dup_opq(px), py, cs, sn, r);
+                h.x = dup_merge(h.x, h2.x);
+                h.y = dup_merge(h.y, h2.y);
+                h.seg |= h2.seg & (int)dup_zero();
+                h.hit = h.hit || (h2.hit && dup_zero() != 0u);
+            }
 #endif
             if (kWaveTree && !stepping) continue;   // the lanes that only helped
             xnx = h.x; xny = h.y; onB = h.hit;
@@ -1148,12 +1202,14 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         bool clipped = false;
         float gnorm = 0.f;
         Jet aj{0.f, 0.f, 0.f, 0.f};
+        WOST_PHASE("sample_and_clip");
         if (SRC) {                                                   // :242-258
             float rs;
             if constexpr (FIX && DELTA)                              // Q4/Q5 fixed: this ball's law
                 rs = sample_rho_screened_fixed(A.table + kFixTableOffset, u01(rn.y), r * sqrt_sb) * r;
             else
                 rs = sample_rho_tail(sT, node0, u01(rn.y)) * r;      // :244 (sampler, quirks Q3-Q5)
+            if (WOST_ABL_DUP & 16) rs = dup_merge(rs, sample_rho_tail(sT, node0, u01(rn.y | dup_zero())) * r);
             if constexpr (FIX && !DELTA) {                           // Q13 fixed: own direction
                 float ts = (u01(rn.w) * 2.0f) * kPiF;
                 if (NEU && onB0) ts = ts / 2.0f + (phi0 - kPiF / 2.0f);   // the inward hemisphere
@@ -1187,13 +1243,25 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 if (clipped) { yx = xnx; yy = xny; }
             }
             if (DELTA) {
+                WOST_PHASE("greens_norm");
                 gnorm = greens_norm_from_table(sG, r * sqrt_sb, r, inv_sb);   // solvers/utils.py:29-44
+                if (WOST_ABL_DUP & 32) gnorm = dup_merge(gnorm, greens_norm_from_table(sG, dup_opq(r) * sqrt_sb, r, inv_sb));
+                WOST_PHASE("alpha_jet");
                 aj = fld.alpha_jet(yx, yy);
+                if (WOST_ABL_DUP & 64) {
+                    const Jet a2 = fld.alpha_jet(dup_opq(yx), yy);
+                    aj.v = dup_merge(aj.v, a2.v);
+                    aj.gx = dup_merge(aj.gx, a2.gx);
+                    aj.gy = dup_merge(aj.gy, a2.gy);
+                    aj.lap = dup_merge(aj.lap, a2.lap);
+                }
             }
+            WOST_PHASE("source_contribution");
             if constexpr (NS == 1) {
                 float c = 0.0f;
                 if (!clipped) {
-                    const float f = fld.f(yx, yy);
+                    float f = fld.f(yx, yy);
+                    if (WOST_ABL_DUP & 256) f = dup_merge(f, fld.f(dup_opq(yx), yy));
                     if (DELTA)
                         c = (f * gnorm) * f_rsq(aj.v * ax) * w;  // :253-254
                     else
@@ -1225,6 +1293,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             rr[1] = float4{yx, yy, cv, SRC ? 1.0f : 0.0f};
         }
 
+        WOST_PHASE("delta_update");
         if (DELTA && FIX) {
             const float mu = u01(rn.z);
             // collision: mu <= sigma_bar |G| and the sample before the ray's boundary point
@@ -1246,7 +1315,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             // only the field evaluations stay divergent
             float anew = aj.v;                                       // collision, or a clipped accept
 #if !defined(WOST_ABL_NO_ALPHA_Z)
-            if (accept && !clipped) anew = fld.alpha(xnx, xny);      // :277
+            if (accept && !clipped) {
+                anew = fld.alpha(xnx, xny);                          // :277
+                if (WOST_ABL_DUP & 128) anew = dup_merge(anew, fld.alpha(dup_opq(xnx), xny));
+            }
 #endif
             float sc = 1.0f;
 #if defined(WOST_ABL_NO_SIGMA_PRIME)
@@ -1254,7 +1326,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #else
             if (!accept) {
 #endif
-                const float spv = sigma_prime_from(aj, fld.sigma(yx, yy), fld.detached());  // :281
+                float spv = sigma_prime_from(aj, fld.sigma(yx, yy), fld.detached());  // :281
+                if (WOST_ABL_DUP & 512)
+                    spv = dup_merge(spv, sigma_prime_from(Jet{dup_opq(aj.v), aj.gx, aj.gy, aj.lap},
+                                                          fld.sigma(dup_opq(yx), yy), fld.detached()));
                 sc = 1.0f - spv * inv_sb;
                 sc = (0.0f > sc) ? 0.0f : sc;                        // Python max(., 0.0) (:282)
             }
@@ -1268,6 +1343,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         }
         k += 1;                                                      // :291
         dD = dd;   // the loop tests the distance of the pre-step point (quirk Q7)
+        WOST_PHASE("loop_head");
     }
 #if defined(WOST_TREE_ITER_STATS)
     // each lane's counters into the workgroup's study words after its pools (the host
