@@ -879,8 +879,20 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     // polylines whose LDS copy would cost the walk kernel its occupancy are read from
     // global memory instead (field-specialised kernels; the precompiled ones stage them)
     // (the staged tree records have their own budget, kTreeLdsMaxBytes)
-    const bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0,
-                                                        jit_const_dirichlet(nd_)) > kGlobalPolylineLdsBytes;
+    bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0,
+                                                  jit_const_dirichlet(nd_)) > kGlobalPolylineLdsBytes;
+    // the brute-force scan of a long Neumann polyline (neumann_scan_both) reads every vertex
+    // at every step: staged in LDS with one 1024-thread workgroup per CU when it fits (a
+    // broadcast LDS read per vertex), else from global memory
+    if (gpoly && h->jit_enabled && jit_fused_neumann_scan(mode, nn_)) {
+        int cap = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device));
+        if (walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0, jit_const_dirichlet(nd_), false, false,
+                           kTreeStageVertsBlock) <= (size_t)cap) {
+            gpoly = false;
+            block = kTreeStageVertsBlock;
+        }
+    }
     auto stage_of = [](int recs, int verts) { return recs > 0 ? (verts > 0 ? 2 : 1) : 0; };
     hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts));
     if (!jfn && block != kWalkBlock) {   // the precompiled kernels run 256-thread workgroups, no staged tree

@@ -959,6 +959,23 @@ WOST_HD float bits_to_float(int32_t b) { return __builtin_bit_cast(float, b); }
 // r = a - q dn (exact, fma), RN(q + r y) -- correctly rounded for every a with
 // 2^-100 <= |a| <= 2 and each of these 65 dn, checked exhaustively on the host
 // (tests/native/unit_dir_check.cpp). Anything else takes the IEEE operations.
+// (n, y) of unit_direction for k = -64..64 (A/B WOST_EXP_UNIT_TAB: one load instead of
+// the bit arithmetic)
+struct UnitDirTab { float v[2 * 129]; };
+constexpr UnitDirTab make_unit_dir_tab() {
+    UnitDirTab t{};
+    for (int k = -64; k <= 64; ++k) {
+        const int32_t kneg = k >> 31, j = ((k >> 1) & ~kneg) | (-((1 - k) >> 1) & kneg);
+        const int32_t jneg = j >> 31;
+        t.v[2 * (k + 64)] = __builtin_bit_cast(float, 0x3F800000 + j);
+        t.v[2 * (k + 64) + 1] = __builtin_bit_cast(float, 0x3F800000 + ((-2 * j) & ~jneg) + (((1 - j) >> 1) & jneg));
+    }
+    return t;
+}
+#if defined(WOST_EXP_UNIT_TAB) && defined(__HIP_DEVICE_COMPILE__)
+__constant__ UnitDirTab kUnitDirTab = make_unit_dir_tab();
+#endif
+
 WOST_HD void unit_direction(float dxi, float dyi, float& dn, float& dx, float& dy) {
 #pragma clang fp contract(off)
     const float s2 = dxi * dxi + dyi * dyi;
@@ -968,11 +985,17 @@ WOST_HD void unit_direction(float dxi, float dyi, float& dn, float& dx, float& d
 #else
     const bool fast = (uint32_t)(k + 64) <= 128u && fabsf(dxi) >= 0x1p-100f && fabsf(dyi) >= 0x1p-100f;
 #endif
+#if defined(WOST_EXP_UNIT_TAB) && defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t ti = (uint32_t)(k + 64) <= 128u ? (uint32_t)(k + 64) : 64u;
+    const float2 nyv = reinterpret_cast<const float2*>(kUnitDirTab.v)[ti];
+    const float n = nyv.x, y = nyv.y;
+#else
     // branch-free selects (the compiler otherwise splits the wave here)
     const int32_t kneg = k >> 31, j = ((k >> 1) & ~kneg) | (-((1 - k) >> 1) & kneg);
     const int32_t jneg = j >> 31;
     const float n = bits_to_float(0x3F800000 + j);
     const float y = bits_to_float(0x3F800000 + ((-2 * j) & ~jneg) + (((1 - j) >> 1) & jneg));
+#endif
     const float qx = dxi * y, qy = dyi * y;
     dn = n;
     dx = fmaf(fmaf(-qx, n, dxi), y, qx);
@@ -1240,6 +1263,136 @@ WOST_HD float silhouette_distance_compact(VP v, SP sv, float px, float py) {
         best = d2 < best ? d2 : best;
     }
     return best == WOST_INF ? best : sqrt_rn(best);
+}
+
+// Both Neumann queries of a step in ONE pass over a long polyline (the brute-force scan,
+// the reference's own algorithm: every segment, :83-102 and :134-197), for polylines
+// that are not compiled in (v in LDS or global memory, wave-uniform index). The step's
+// direction is drawn first (it does not depend on the silhouette distance; r enters the
+// ray query only at its finish, scan_both_finish). Per vertex: the silhouette cross
+// products of silhouette_distance (the same operands and rounding) and the per-vertex
+// line filter of intersect_polylines_lines (threshold S = 2^-17 (c1 + |q|_1), c1 >=
+// max |v_i|_1); the rare work -- a silhouette vertex's squared distance, a candidate
+// segment's exact test (ray_segment_time_filtered, ascending, so `s < best` keeps the
+// first argmin) -- runs only when some lane of the wave needs it. Bit for bit
+// silhouette_distance and intersect_polylines<false>; four vertices per loaded batch.
+struct ScanBoth {
+    float d2;          // the least squared distance to a silhouette vertex (INF: none)
+    float best;        // the ray query's least segment parameter s (INF: no crossing)
+    int bi;            // its segment
+    float dx, dy, qx, qy;   // the unit direction and the ray's origin q = p + 1e-6 d
+    bool degenerate;   // |d| < 1e-10: no ray query
+};
+// SCALAR (a polyline in global memory, GL kernels): the vertices through the scalar unit
+// (constant address space, wave-uniform index: s_load of four vertices at a time, the
+// next batch requested before the current one is scanned) instead of a vector load per
+// vertex and lane.
+template <bool SCALAR = false, class VP>
+WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py, float dxi, float dyi) {
+#pragma clang fp contract(off)
+#if defined(__HIP_DEVICE_COMPILE__)
+    using CV = const __attribute__((address_space(4))) float2*;
+    const auto v = [&]() {
+        if constexpr (SCALAR) return (CV)(const float2*)vin;
+        else return vin;
+    }();
+#else
+    const auto v = vin;
+#endif
+    ScanBoth o;
+    float dn;
+    unit_direction(dxi, dyi, dn, o.dx, o.dy);
+    o.degenerate = dn < 1e-10f;
+    const float dx = o.dx, dy = o.dy;
+    o.qx = px + 1e-6f * dx;
+    o.qy = py + 1e-6f * dy;
+    const float qx = o.qx, qy = o.qy;
+    const float m = fmaf(dx, qy, -(dy * qx));                              // cross(d, q)
+    const float S = 7.62939453125e-06f * (c1 + (fabsf(qx) + fabsf(qy)));   // 2^-17
+    const float hi = m + S, lo = m - S;
+    float d2best = WOST_INF, best = WOST_INF;
+    int bi = -1;
+    float2 b = v[0];
+    bool aprev, bprev;
+    {
+        const float c = fmaf(dx, b.y, -(dy * b.x));
+        aprev = c > hi;
+        bprev = c < lo;
+    }
+    float cprev = 0.0f;
+    // vertex j+1 closes segment j (b = v[j] -> c = v[j+1]) and, for 1 <= j <= nv-2,
+    // decides whether v[j] is a silhouette vertex (segments j-1 and j); the next batch of
+    // four vertices is loaded (one 32-byte load while it lies inside the polyline) before
+    // the current one is scanned
+    struct Quad { float2 a, b, c, d; };
+    auto load4 = [&](int i, float2* q) {   // vertices i .. i+3, clamped to nv - 1
+        if (i + 3 < nv) {
+            Quad w;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if constexpr (SCALAR) w = *(const __attribute__((address_space(4))) Quad*)(&v[i]);
+            else w = *(const Quad*)(&v[i]);
+#else
+            w = *(const Quad*)(&v[i]);
+#endif
+            q[0] = w.a; q[1] = w.b; q[2] = w.c; q[3] = w.d;
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) q[u] = v[i + u < nv ? i + u : nv - 1];
+        }
+    };
+    float2 nxt[4];
+    load4(1, nxt);
+    for (int j0 = 0; j0 + 1 < nv; j0 += 4) {
+        float2 cs[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cs[u] = nxt[u];
+        load4(j0 + 5, nxt);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u;
+            if (j + 1 < nv) {
+                const float2 c = cs[u];
+                // silhouette (silhouette_distance's operands: x - b, then the cross product)
+                const float bpx = px - b.x, bpy = py - b.y;
+                const float ccur = (c.x - b.x) * bpy - (c.y - b.y) * bpx;
+                const bool sil = j >= 1 && cprev * ccur < 0.0f;
+                if (sil) {   // (no lane: s_cbranch_execz skips the block)
+                    const float d2 = bpx * bpx + bpy * bpy;
+                    d2best = d2 < d2best ? d2 : d2best;
+                }
+                cprev = ccur;
+                // ray filter on the vertex, candidate segment j
+                const float lc = fmaf(dx, c.y, -(dy * c.x));
+                const bool ah = lc > hi, bl = lc < lo;
+                const bool cand = !((aprev && ah) || (bprev && bl));
+                if (cand) {
+                    const float s = ray_segment_time_filtered(b, c, qx, qy, dx, dy);
+                    if (s < best) { best = s; bi = j; }
+                }
+                aprev = ah;
+                bprev = bl;
+                b = c;
+            }
+        }
+    }
+    o.d2 = nv < 3 ? WOST_INF : d2best;
+    o.best = best;
+    o.bi = bi;
+    return o;
+}
+
+// The silhouette distance of a neumann_scan_both pass (silhouette_distance's result).
+WOST_HD float scan_both_silhouette(const ScanBoth& o) { return o.d2 == WOST_INF ? o.d2 : sqrt_rn(o.d2); }
+
+// The ray query's hit (intersect_polylines<false>'s result) once r is known.
+template <class VP>
+WOST_HD Hit scan_both_finish(VP v, const ScanBoth& o, float px, float py, float r) {
+    if (o.degenerate) {
+        Hit h;
+        h.x = px; h.y = py; h.nx = 1.f; h.ny = 0.f; h.hit = false; h.seg = -1;
+        return h;
+    }
+    return intersect_finish<false>(v, o.bi, o.best, px, py, o.dx, o.dy, o.qx, o.qy, r);
 }
 
 // ---------------------------------------------------------------------------

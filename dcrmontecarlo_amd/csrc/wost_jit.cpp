@@ -381,6 +381,12 @@ bool jit_const_neumann(int mode, int nn) {
     return mode_neu(mode) && !mode_tree(mode) && nn >= 1 && nn <= jit_const_vertices();
 }
 
+bool jit_fused_neumann_scan(int mode, int nn) {
+    // (WOST_EXP_FLAGS 2^28: the two separate scans, A/B)
+    return mode_neu(mode) && !mode_tree(mode) && !mode_fix(mode) && !jit_const_neumann(mode, nn) && nn >= 66 &&
+           !(exp_flags() & (1 << 28));
+}
+
 std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources,
                          int block, const float* seg_phi, bool global_polylines, int tree_stage,
@@ -403,7 +409,8 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 65536) o << "#define WOST_ABL_NO_SILHOUETTE 1\n";
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
-    if (exp_flags() >> 18) o << "#define WOST_ABL_DUP " << (exp_flags() >> 18) << "\n";   // phase_dup.sh
+    if (exp_flags() & (1 << 29)) o << "#define WOST_EXP_UNIT_TAB 1\n";   // A/B: unit_direction's (n, y) table
+    if ((exp_flags() >> 18) & 1023) o << "#define WOST_ABL_DUP " << ((exp_flags() >> 18) & 1023) << "\n";   // phase_dup.sh
     o << "#define WOST_JIT_TRIG_EXACT " << (exact_trig ? 1 : 0) << "\n";   // wost_set_trig
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
     if (const char* e = std::getenv("WOST_JIT_PHILOX_AHEAD"))   // A/B: Philox one step ahead
@@ -461,6 +468,22 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     const bool nconst = jit_const_neumann(mode, nn) && (seg_phi != nullptr || nn < 2);
     o << "    static constexpr bool kConstDirichlet = " << (dconst ? "true" : "false") << ";\n";
     o << "    static constexpr bool kConstNeumann = " << (nconst ? "true" : "false") << ";\n";
+    // a long Neumann polyline scanned (no segment tree: the brute-force kernel): both
+    // queries in one pass with the per-vertex line filter (neumann_scan_both);
+    // WOST_EXP_FLAGS 2^28: the two separate scans instead (A/B)
+    const bool fused = !nconst && jit_fused_neumann_scan(mode, nn);
+    o << "    static constexpr bool kFusedNeumann = " << (fused ? "true" : "false") << ";\n";
+    if (fused) {
+        float c1 = 0.0f;
+        for (int i = 0; i < nn; ++i) c1 = std::max(c1, std::fabs(nverts[2 * i]) + std::fabs(nverts[2 * i + 1]));
+        o << "    __device__ __forceinline__ wost::ScanBoth neumann_scan_both(const float2* sN, int nn, float x, float y,"
+             " float dx, float dy) const {\n"
+          << "        return wost::neumann_scan_both<" << (global_polylines ? "true" : "false") << ">(sN, nn, "
+          << lit(c1 * 1.0001f) << ", x, y, dx, dy);\n    }\n";
+    } else {
+        o << "    __device__ __forceinline__ wost::ScanBoth neumann_scan_both(const float2*, int, float, float, float,"
+             " float) const { return wost::ScanBoth{}; }\n";
+    }
     o << "    __device__ __forceinline__ float dirichlet_distance(const float2* sD, int nd, float x, float y) const {\n";
     if (dconst) {
         o << "        const float2 v[" << nd << "] = {";

@@ -26,6 +26,9 @@ int jit_const_vertices();
 // Which polylines a specialised kernel of `mode` compiles in.
 bool jit_const_dirichlet(int nd);
 bool jit_const_neumann(int mode, int nn);
+// a long Neumann polyline scanned without the segment tree (the brute-force kernel, reference
+// mode): both queries of a step in one pass (wost_device.h neumann_scan_both)
+bool jit_fused_neumann_scan(int mode, int nn);
 
 // HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
 // (wost_internal.h WalkMode) with the fields of `prog` and short polylines

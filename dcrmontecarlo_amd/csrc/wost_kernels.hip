@@ -81,6 +81,7 @@ struct ProgView {
 struct InterpFields {
     static constexpr bool kConstDirichlet = false;   // polylines are staged in LDS
     static constexpr bool kConstNeumann = false;
+    static constexpr bool kFusedNeumann = false;      // (the field-specialised kernels' long-polyline scan)
     ProgView P;
     DField fG, fF, fS, fA;
     bool det;

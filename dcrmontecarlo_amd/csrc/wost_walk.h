@@ -1136,15 +1136,26 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         };
         float r;
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
+        // a long polyline's brute-force scans in one pass (neumann_scan_both): the direction
+        // first, the ray query's finish after r
+        constexpr bool kFused = NEU && !TREE && !FIX && F::kFusedNeumann;
+        ScanBoth sb{};
         WOST_PHASE("silhouette");
         if (NEU) {
 #if defined(WOST_ABL_NO_SILHOUETTE)   // ablation (timing only)
             const float dn = WOST_INF;
 #else
-            const float dn = kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane,
-                                                                       WOST_IC)
-                           : TREE      ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
-                                       : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
+            float dn;
+            if constexpr (kFused) {
+                draw_direction();
+                sb = fld.neumann_scan_both(nP, A.nn, px, py, cs, sn);
+                dn = scan_both_silhouette(sb);                        // :211
+            } else {
+                dn = kWaveTree ? silhouette_distance_tree_wave(tree, px, py, dd, A.tree_stop2, stepping, tws, lane,
+                                                               WOST_IC)
+                     : TREE    ? silhouette_distance_tree(tree, px, py, dd, A.tree_stop2)
+                               : fld.neumann_silhouette_distance(nP, A.nn, px, py);  // :211
+            }
 #endif
             dnv = dn;
             const float m = dn < dd ? dn : dd;                       // Python min()
@@ -1153,7 +1164,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             r = dd > A.rmin ? dd : A.rmin;                           // :215
         }
         WOST_PHASE("philox_direction");
-        draw_direction();
+        if (!kFused) draw_direction();
 #if !defined(WOST_ABL_NO_PHILOX)
         if (WOST_PHILOX_AHEAD) {   // the next step's words, overlapping this step's arithmetic
             uint32_t key0 = A.key0, key1 = A.key1;
@@ -1170,11 +1181,12 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #if defined(WOST_ABL_NO_RAY)
             Hit h; h.x = px + r * cs; h.y = py + r * sn; h.hit = false; h.seg = -1;
 #else
-            Hit h = kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws,
-                                                                          lane, WOST_IC)
+            Hit h = kFused    ? scan_both_finish(nP, sb, px, py, r)
+                    : kWaveTree ? intersect_polylines_tree_wave<false, FIX>(tree, px, py, cs, sn, r, stepping, tws,
+                                                                            lane, WOST_IC)
                     : FIX       ? fld.neumann_intersect_nearest(nP, A.nn, px, py, cs, sn, r)
                                 : fld.neumann_intersect(nP, A.nn, px, py, cs, sn, r);
-            if ((WOST_ABL_DUP & 8) && !kWaveTree && !FIX) {
+            if ((WOST_ABL_DUP & 8) && !kWaveTree && !FIX && !kFused) {
                 const Hit h2 = fld.neumann_intersect(nP, A.nn, dup_opq(px), py, cs, sn, r);
                 h.x = dup_merge(h.x, h2.x);
                 h.y = dup_merge(h.y, h2.y);

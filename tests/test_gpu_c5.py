@@ -205,3 +205,35 @@ def test_c5_walk_pools_change_no_bits_in_walk_range_solves(gpu_available, monkey
         out.append(s.solve_range(pts, 8192, 4096, 8192, sc.max_steps, sc.eps, 21))
     assert out[0].shape[0] == len(pts)
     np.testing.assert_array_equal(out[1], out[0])
+
+
+@pytest.mark.parametrize("name", ["wenner_topography", "wenner_topography_physical"])
+def test_c5_fused_bruteforce_scan_equals_separate_scans(gpu_available, name):
+    """The brute-force scan kernel (set_segment_tree(-1)) runs both Neumann queries of a
+    step in one pass with the per-vertex line filter (wost_device.h neumann_scan_both):
+    walk for walk the bits of the two separate full scans (WOST_EXP_FLAGS 2^28, the
+    round-4 kernel) and of the segment tree."""
+    import os
+
+    from dcrmontecarlo_amd import scenarios as S
+
+    sc = S.ALL[name](n_electrodes=64, n_walks=1)
+    pts = sc.points[::2]
+    runs = {}
+    for label, flags in (("fused", None), ("separate", str(1 << 28)), ("tree", None)):
+        old = os.environ.pop("WOST_EXP_FLAGS", None)
+        if flags:
+            os.environ["WOST_EXP_FLAGS"] = flags
+        try:
+            s = sc.solver(device=0)
+            if label != "tree":
+                s.set_segment_tree(-1)
+            runs[label] = s.solve_walks(pts, nWalks=512, maxSteps=sc.max_steps, eps=sc.eps, seed=29)
+            assert s.last_timing["tree"] == (1 if label == "tree" else 0)
+        finally:
+            os.environ.pop("WOST_EXP_FLAGS", None)
+            if old is not None:
+                os.environ["WOST_EXP_FLAGS"] = old
+    for label in ("separate", "tree"):
+        np.testing.assert_array_equal(runs["fused"][1], runs[label][1], err_msg=label)
+        np.testing.assert_array_equal(runs["fused"][0].view(np.uint32), runs[label][0].view(np.uint32), err_msg=label)
