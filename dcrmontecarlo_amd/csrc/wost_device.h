@@ -1341,12 +1341,19 @@ WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py,
         }
     };
     float2 nxt[4];
-    load4(1, nxt);
+    if constexpr (SCALAR) load4(1, nxt);
     for (int j0 = 0; j0 + 1 < nv; j0 += 4) {
         float2 cs[4];
+        if constexpr (SCALAR) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) cs[u] = nxt[u];
-        load4(j0 + 5, nxt);
+            for (int u = 0; u < 4; ++u) cs[u] = nxt[u];
+            load4(j0 + 5, nxt);
+        } else {
+            // LDS (the staged copy): vertices past the last are the staged data after it
+            // (or 0 beyond the allocation), read but never used
+#pragma unroll
+            for (int u = 0; u < 4; ++u) cs[u] = v[j0 + 1 + u];
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int j = j0 + u;
@@ -1357,6 +1364,7 @@ WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py,
                 const float ccur = (c.x - b.x) * bpy - (c.y - b.y) * bpx;
                 const bool sil = j >= 1 && cprev * ccur < 0.0f;
                 if (sil) {   // (no lane: s_cbranch_execz skips the block)
+                    WOST_NO_SPECULATION();   // a real branch: rarely taken, not worth 4 VALU per vertex
                     const float d2 = bpx * bpx + bpy * bpy;
                     d2best = d2 < d2best ? d2 : d2best;
                 }
