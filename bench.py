@@ -689,7 +689,7 @@ def wenner_main(args, world, rank, local):
                                          "walk_steps": steps_local})
     res_phys = None
     pm = ph = None
-    if args.fields == "literal":   # outside the timed region: the physical survey's rho_a
+    if args.fields == "literal" and not args.no_rho:   # outside the timed region: the physical survey's rho_a
         sp = S.wenner_topography(n_electrodes=E, n_walks=W1, physical=True)
         pm = sp.solver(device=local)
         ph = survey.homogeneous_solver(sp, WENNER_ALPHA_BG, pm, device=local)
@@ -774,12 +774,15 @@ def wenner_main(args, world, rank, local):
 
         if args.fields == "physical":
             out["rho_a"] = rho_summary(res, f"the timed survey ({sc.name})")
+        elif res_phys is None:
+            out["rho_a"] = None   # --no-rho (profiling runs)
+            out["rho_a_literal_timed_survey"] = rho_summary(res, sc.name)
         else:
             out["rho_a"] = rho_summary(res_phys, f"wenner_topography_physical, {Wt} walks per electrode, untimed "
                                                  "(the literal fields put the electrodes in 'air': "
                                                  "their rho_a is not physical)")
             out["rho_a_literal_timed_survey"] = rho_summary(res, sc.name)
-        if E == 256:
+        if E == 256 and not args.no_rho:
             # deterministic parity: the reference's own C5 Wenner survey replayed on the Philox
             # stream (16 quadripoles x both receivers x 64 walks, physical model + background)
             # against the device on the same walks

@@ -1276,6 +1276,8 @@ WOST_HD float silhouette_distance_compact(VP v, SP sv, float px, float py) {
 // segment's exact test (ray_segment_time_filtered, ascending, so `s < best` keeps the
 // first argmin) -- runs only when some lane of the wave needs it. Bit for bit
 // silhouette_distance and intersect_polylines<false>; four vertices per loaded batch.
+template <bool B> struct BoolC { static constexpr bool value = B; };   // a compile-time flag argument
+
 struct ScanBoth {
     float d2;          // the least squared distance to a silhouette vertex (INF: none)
     float best;        // the ray query's least segment parameter s (INF: no crossing)
@@ -1283,9 +1285,8 @@ struct ScanBoth {
     float dx, dy, qx, qy;   // the unit direction and the ray's origin q = p + 1e-6 d
     bool degenerate;   // |d| < 1e-10: no ray query
 };
-// SCALAR (a polyline in global memory, GL kernels): the vertices through the scalar unit
-// (constant address space, wave-uniform index: s_load of four vertices at a time, the
-// next batch requested before the current one is scanned) instead of a vector load per
+// SCALAR (a polyline in global memory, GL kernels): the batch's vertices through the
+// scalar unit (constant address space, wave-uniform index) instead of a vector load per
 // vertex and lane.
 template <bool SCALAR = false, class VP>
 WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py, float dxi, float dyi) {
@@ -1321,68 +1322,61 @@ WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py,
     }
     float cprev = 0.0f;
     // vertex j+1 closes segment j (b = v[j] -> c = v[j+1]) and, for 1 <= j <= nv-2,
-    // decides whether v[j] is a silhouette vertex (segments j-1 and j); the next batch of
-    // four vertices is loaded (one 32-byte load while it lies inside the polyline) before
-    // the current one is scanned
-    struct Quad { float2 a, b, c, d; };
-    auto load4 = [&](int i, float2* q) {   // vertices i .. i+3, clamped to nv - 1
-        if (i + 3 < nv) {
-            Quad w;
-#if defined(__HIP_DEVICE_COMPILE__)
-            if constexpr (SCALAR) w = *(const __attribute__((address_space(4))) Quad*)(&v[i]);
-            else w = *(const Quad*)(&v[i]);
-#else
-            w = *(const Quad*)(&v[i]);
-#endif
-            q[0] = w.a; q[1] = w.b; q[2] = w.c; q[3] = w.d;
-        } else {
+    // decides whether v[j] is a silhouette vertex (segments j-1 and j). Batches of eight
+    // vertices: the per-vertex tests only set a lane's bits (silhouette vertex, candidate
+    // segment), and the rare work runs once per batch for the lanes with bits set --
+    // one branch per eight vertices instead of two per vertex
+    constexpr int kB = 8;
+    auto batch = [&](int j0, auto check) {
+        constexpr bool kCheck = decltype(check)::value;   // the last, partial batch
+        float2 cs[kB];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) q[u] = v[i + u < nv ? i + u : nv - 1];
+        for (int u = 0; u < kB; ++u) {
+            if constexpr (SCALAR) cs[u] = v[!kCheck || j0 + 1 + u < nv ? j0 + 1 + u : nv - 1];
+            else cs[u] = v[j0 + 1 + u];   // LDS (the staged copy): past the last vertex the staged
+                                          // data after it (or 0 beyond the allocation), unused
         }
-    };
-    float2 nxt[4];
-    if constexpr (SCALAR) load4(1, nxt);
-    for (int j0 = 0; j0 + 1 < nv; j0 += 4) {
-        float2 cs[4];
-        if constexpr (SCALAR) {
+        uint32_t silm = 0u, candm = 0u;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) cs[u] = nxt[u];
-            load4(j0 + 5, nxt);
-        } else {
-            // LDS (the staged copy): vertices past the last are the staged data after it
-            // (or 0 beyond the allocation), read but never used
-#pragma unroll
-            for (int u = 0; u < 4; ++u) cs[u] = v[j0 + 1 + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kB; ++u) {
             const int j = j0 + u;
-            if (j + 1 < nv) {
+            if (!kCheck || j + 1 < nv) {
                 const float2 c = cs[u];
                 // silhouette (silhouette_distance's operands: x - b, then the cross product)
                 const float bpx = px - b.x, bpy = py - b.y;
                 const float ccur = (c.x - b.x) * bpy - (c.y - b.y) * bpx;
-                const bool sil = j >= 1 && cprev * ccur < 0.0f;
-                if (sil) {   // (no lane: s_cbranch_execz skips the block)
-                    WOST_NO_SPECULATION();   // a real branch: rarely taken, not worth 4 VALU per vertex
-                    const float d2 = bpx * bpx + bpy * bpy;
-                    d2best = d2 < d2best ? d2 : d2best;
-                }
+                if ((kCheck || u > 0 || j0 > 0) ? (j >= 1 && cprev * ccur < 0.0f) : false) silm |= 1u << u;
                 cprev = ccur;
                 // ray filter on the vertex, candidate segment j
                 const float lc = fmaf(dx, c.y, -(dy * c.x));
                 const bool ah = lc > hi, bl = lc < lo;
-                const bool cand = !((aprev && ah) || (bprev && bl));
-                if (cand) {
-                    const float s = ray_segment_time_filtered(b, c, qx, qy, dx, dy);
-                    if (s < best) { best = s; bi = j; }
-                }
+                if (!((aprev && ah) || (bprev && bl))) candm |= 1u << u;
                 aprev = ah;
                 bprev = bl;
                 b = c;
             }
         }
-    }
+        if ((silm | candm) != 0u) {   // (no lane: s_cbranch_execz skips the block)
+            WOST_NO_SPECULATION();
+            while (silm != 0u) {      // the squared distances of this lane's silhouette vertices
+                const int u = __builtin_ctz(silm);
+                silm &= silm - 1u;
+                const float2 bb = v[j0 + u];
+                const float bpx = px - bb.x, bpy = py - bb.y;
+                const float d2 = bpx * bpx + bpy * bpy;
+                d2best = d2 < d2best ? d2 : d2best;
+            }
+            while (candm != 0u) {     // its candidate segments, ascending: `s < best` keeps the first argmin
+                const int u = __builtin_ctz(candm);
+                candm &= candm - 1u;
+                const float s = ray_segment_time_filtered(v[j0 + u], v[j0 + u + 1], qx, qy, dx, dy);
+                if (s < best) { best = s; bi = j0 + u; }
+            }
+        }
+    };
+    const int nfull = (nv - 1) / kB * kB;   // segments in whole batches
+    for (int j0 = 0; j0 < nfull; j0 += kB) batch(j0, BoolC<false>{});
+    if (nfull < nv - 1) batch(nfull, BoolC<true>{});
     o.d2 = nv < 3 ? WOST_INF : d2best;
     o.best = best;
     o.bi = bi;

@@ -31,6 +31,8 @@ def lib(tmp_path_factory):
     fp = ctypes.POINTER(ctypes.c_float)
     lb.scan_check.argtypes = [fp, ctypes.c_int, fp, fp, fp, ctypes.c_long, ctypes.POINTER(ctypes.c_long)]
     lb.scan_check.restype = ctypes.c_int
+    lb.scan_both_check.argtypes = lb.scan_check.argtypes
+    lb.scan_both_check.restype = ctypes.c_int
     return lb
 
 
@@ -86,3 +88,31 @@ def test_two_pass_compiled_scans_match_one_pass(lib, shape):
     assert out[0] == 0 and out[1] == 0, list(out)
     assert out[2] > 1000, list(out)                       # the ray query exercised
     assert out[3] > 1000 or shape == "flat65", list(out)  # (a straight line has no silhouette)
+
+
+def _long_shapes():
+    from dcrmontecarlo_amd import scenarios as S
+
+    rng = np.random.default_rng(1)
+    th = np.linspace(0, 2 * np.pi, 2001)
+    wig = np.stack([np.cos(th) * (1 + 0.05 * np.sin(37 * th)), np.sin(th) * (1 + 0.05 * np.sin(37 * th))], 1) * 40.0
+    return {"topography10k": S.topography(10_000), "wiggly_circle2001": wig,
+            "random_walk1003": np.cumsum(rng.normal(size=(1003, 2)), 0),
+            "flat66": np.stack([np.linspace(-1e3, 1e3, 66), np.zeros(66)], 1),
+            "zigzag67": np.stack([np.arange(67.0), (np.arange(67) % 2) * 3.0], 1)}
+
+
+@pytest.mark.parametrize("shape", list(_long_shapes()))
+def test_fused_bruteforce_scan_matches_both_scans(lib, shape):
+    """neumann_scan_both (the brute-force kernels' one pass over a long polyline, batches of
+    eight vertices, the last one partial) returns silhouette_distance's and
+    intersect_polylines<false>'s bits."""
+    V = np.ascontiguousarray(_long_shapes()[shape], np.float32)
+    rng = np.random.default_rng(len(V) + 7)
+    pts, dirs, radii = _queries(rng, V.astype(np.float64), 4000 if len(V) > 5000 else 20_000)
+    out = (ctypes.c_long * 4)()
+    p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    assert lib.scan_both_check(p(V), len(V), p(pts), p(dirs), p(radii), len(pts), out) == 0
+    assert out[0] == 0 and out[1] == 0, list(out)
+    assert out[2] > 200, list(out)
+    assert out[3] > 200 or shape == "flat66", list(out)
