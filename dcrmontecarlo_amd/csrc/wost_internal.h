@@ -96,8 +96,6 @@ hipError_t launch_geometry_tree_query(int op, const float2* verts, int nv, const
                                       const float2* dirs, const float* radii, int64_t n, float* out_f,
                                       hipStream_t s);
 
-// atan2 of the left normal of each of the nseg segments of verts -> phi[nseg].
-
 hipError_t launch_eval_field(const char* prog, int which, const float2* pts, int64_t n,
                              float4* out, hipStream_t s);
 

@@ -237,3 +237,22 @@ def test_c5_fused_bruteforce_scan_equals_separate_scans(gpu_available, name):
     for label in ("separate", "tree"):
         np.testing.assert_array_equal(runs["fused"][1], runs[label][1], err_msg=label)
         np.testing.assert_array_equal(runs["fused"][0].view(np.uint32), runs[label][0].view(np.uint32), err_msg=label)
+
+
+def test_fused_bruteforce_scan_from_global_memory(gpu_available):
+    """A Neumann polyline too long to stage in LDS even with one 1024-thread workgroup per
+    CU (20,000 segments: 160 KB of vertices) is scanned from global memory through the
+    scalar unit (neumann_scan_both<SCALAR>): walk for walk the segment tree's bits."""
+    from dcrmontecarlo_amd import scenarios as S
+
+    sc = S.wenner_topography(n_electrodes=32, n_walks=1, n_segments=20_000)
+    pts = sc.points[::2]
+    runs = {}
+    for label in ("scan", "tree"):
+        s = sc.solver(device=0)
+        if label == "scan":
+            s.set_segment_tree(-1)
+        runs[label] = s.solve_walks(pts, nWalks=128, maxSteps=sc.max_steps, eps=sc.eps, seed=31)
+        assert s.last_timing["tree"] == (1 if label == "tree" else 0)
+    np.testing.assert_array_equal(runs["scan"][1], runs["tree"][1])
+    np.testing.assert_array_equal(runs["scan"][0].view(np.uint32), runs["tree"][0].view(np.uint32))

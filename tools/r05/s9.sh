@@ -16,3 +16,5 @@ echo "scan ab rc=$?" >> $O/status.txt
 timeout -k 10 600 python bench.py --workload wenner_topography --steps 3 --warmup 1 --no-cpu > $O/bench_c5.log 2>&1
 echo "bench c5 rc=$?" >> $O/status.txt
 cat $O/status.txt
+timeout -k 10 600 python -u tools/r05/trig_parity.py > gpurun_out/r05s9/trig_parity.log 2>&1
+echo "trig parity rc=$?" >> gpurun_out/r05s9/status.txt
