@@ -1274,8 +1274,8 @@ WOST_HD float silhouette_distance_compact(VP v, SP sv, float px, float py) {
 // line filter of intersect_polylines_lines (threshold S = 2^-17 (c1 + |q|_1), c1 >=
 // max |v_i|_1); the rare work -- a silhouette vertex's squared distance, a candidate
 // segment's exact test (ray_segment_time_filtered, ascending, so `s < best` keeps the
-// first argmin) -- runs only when some lane of the wave needs it. Bit for bit
-// silhouette_distance and intersect_polylines<false>; four vertices per loaded batch.
+// first argmin) -- runs only when some lane of the wave needs it, once per batch of
+// eight vertices. Bit for bit silhouette_distance and intersect_polylines<false>.
 template <bool B> struct BoolC { static constexpr bool value = B; };   // a compile-time flag argument
 
 struct ScanBoth {
@@ -1314,19 +1314,74 @@ WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py,
     float d2best = WOST_INF, best = WOST_INF;
     int bi = -1;
     float2 b = v[0];
+    float cprev = 0.0f;   // (0 at vertex 0: 0 * ccur is never < 0, the j >= 1 guard)
+    // vertex j+1 closes segment j (b = v[j] -> c = v[j+1]) and, for 1 <= j <= nv-2,
+    // decides whether v[j] is a silhouette vertex (segments j-1 and j). Batches of eight
+    // vertices, one branch per batch instead of two per vertex
+    constexpr int kB = 8;
+#if defined(WOST_EXP_SCAN_BITS)
+    // A/B (round-5 first version): the per-vertex tests set a lane's bits (silhouette
+    // vertex, candidate segment) and the rare work runs once per batch for those bits
     bool aprev, bprev;
     {
         const float c = fmaf(dx, b.y, -(dy * b.x));
         aprev = c > hi;
         bprev = c < lo;
     }
-    float cprev = 0.0f;
-    // vertex j+1 closes segment j (b = v[j] -> c = v[j+1]) and, for 1 <= j <= nv-2,
-    // decides whether v[j] is a silhouette vertex (segments j-1 and j). Batches of eight
-    // vertices: the per-vertex tests only set a lane's bits (silhouette vertex, candidate
-    // segment), and the rare work runs once per batch for the lanes with bits set --
-    // one branch per eight vertices instead of two per vertex
-    constexpr int kB = 8;
+    auto batch = [&](int j0, auto check) {
+        constexpr bool kCheck = decltype(check)::value;   // the last, partial batch
+        float2 cs[kB];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            if constexpr (SCALAR) cs[u] = v[!kCheck || j0 + 1 + u < nv ? j0 + 1 + u : nv - 1];
+            else cs[u] = v[j0 + 1 + u];
+        }
+        uint32_t silm = 0u, candm = 0u;
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int j = j0 + u;
+            if (!kCheck || j + 1 < nv) {
+                const float2 c = cs[u];
+                const float bpx = px - b.x, bpy = py - b.y;
+                const float ccur = (c.x - b.x) * bpy - (c.y - b.y) * bpx;
+                if (cprev * ccur < 0.0f) silm |= 1u << u;
+                cprev = ccur;
+                const float lc = fmaf(dx, c.y, -(dy * c.x));
+                const bool ah = lc > hi, bl = lc < lo;
+                if (!((aprev && ah) || (bprev && bl))) candm |= 1u << u;
+                aprev = ah;
+                bprev = bl;
+                b = c;
+            }
+        }
+        if ((silm | candm) != 0u) {
+            WOST_NO_SPECULATION();
+            while (silm != 0u) {
+                const int u = __builtin_ctz(silm);
+                silm &= silm - 1u;
+                const float2 bb = v[j0 + u];
+                const float bpx = px - bb.x, bpy = py - bb.y;
+                const float d2 = bpx * bpx + bpy * bpy;
+                d2best = d2 < d2best ? d2 : d2best;
+            }
+            while (candm != 0u) {
+                const int u = __builtin_ctz(candm);
+                candm &= candm - 1u;
+                const float s = ray_segment_time_filtered(v[j0 + u], v[j0 + u + 1], qx, qy, dx, dy);
+                if (s < best) { best = s; bi = j0 + u; }
+            }
+        }
+    };
+#else
+    // Per vertex only what decides whether the batch holds ANY of this lane's rare work:
+    // the minimum of cprev * ccur (< 0 iff a silhouette vertex), and the minimum and
+    // maximum line distance of the batch's nine vertices (a candidate segment -- one
+    // whose endpoints are not both above nor both below the band -- exists iff the
+    // vertices are not all above and not all below it). A lane with rare work runs the
+    // batch's exact per-vertex tests again from the batch's starting state (~4% of the
+    // batches of a wave on C5). A NaN vertex drops out of the minimum / maximum; its
+    // segments' exact tests never hit (ray_segment_time_filtered), so the result is the same.
+    float lprev = fmaf(dx, b.y, -(dy * b.x));   // the previous vertex's line distance
     auto batch = [&](int j0, auto check) {
         constexpr bool kCheck = decltype(check)::value;   // the last, partial batch
         float2 cs[kB];
@@ -1336,44 +1391,52 @@ WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py,
             else cs[u] = v[j0 + 1 + u];   // LDS (the staged copy): past the last vertex the staged
                                           // data after it (or 0 beyond the allocation), unused
         }
-        uint32_t silm = 0u, candm = 0u;
+        const float2 b0 = b;
+        const float cprev0 = cprev, lprev0 = lprev;
+        float pmin = 0.0f, lmin = lprev, lmax = lprev;
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            const int j = j0 + u;
-            if (!kCheck || j + 1 < nv) {
+            if (!kCheck || j0 + u + 1 < nv) {
                 const float2 c = cs[u];
                 // silhouette (silhouette_distance's operands: x - b, then the cross product)
                 const float bpx = px - b.x, bpy = py - b.y;
                 const float ccur = (c.x - b.x) * bpy - (c.y - b.y) * bpx;
-                if ((kCheck || u > 0 || j0 > 0) ? (j >= 1 && cprev * ccur < 0.0f) : false) silm |= 1u << u;
+                pmin = fminf(pmin, cprev * ccur);
                 cprev = ccur;
-                // ray filter on the vertex, candidate segment j
-                const float lc = fmaf(dx, c.y, -(dy * c.x));
-                const bool ah = lc > hi, bl = lc < lo;
-                if (!((aprev && ah) || (bprev && bl))) candm |= 1u << u;
-                aprev = ah;
-                bprev = bl;
+                const float lc = fmaf(dx, c.y, -(dy * c.x));   // ray filter on the vertex
+                lmin = fminf(lmin, lc);
+                lmax = fmaxf(lmax, lc);
+                lprev = lc;
                 b = c;
             }
         }
-        if ((silm | candm) != 0u) {   // (no lane: s_cbranch_execz skips the block)
+        if (pmin < 0.0f || !(lmin > hi || lmax < lo)) {   // (no lane: s_cbranch_execz skips it)
             WOST_NO_SPECULATION();
-            while (silm != 0u) {      // the squared distances of this lane's silhouette vertices
-                const int u = __builtin_ctz(silm);
-                silm &= silm - 1u;
-                const float2 bb = v[j0 + u];
-                const float bpx = px - bb.x, bpy = py - bb.y;
-                const float d2 = bpx * bpx + bpy * bpy;
-                d2best = d2 < d2best ? d2 : d2best;
-            }
-            while (candm != 0u) {     // its candidate segments, ascending: `s < best` keeps the first argmin
-                const int u = __builtin_ctz(candm);
-                candm &= candm - 1u;
-                const float s = ray_segment_time_filtered(v[j0 + u], v[j0 + u + 1], qx, qy, dx, dy);
-                if (s < best) { best = s; bi = j0 + u; }
+            float2 a = b0;
+            float cp = cprev0, la = lprev0;
+            for (int u = 0; u < kB; ++u) {
+                const int j = j0 + u;
+                if (!kCheck || j + 1 < nv) {
+                    const float2 c = v[j + 1];
+                    const float bpx = px - a.x, bpy = py - a.y;
+                    const float ccur = (c.x - a.x) * bpy - (c.y - a.y) * bpx;
+                    if (cp * ccur < 0.0f) {   // v[j] a silhouette vertex: its squared distance
+                        const float d2 = bpx * bpx + bpy * bpy;
+                        d2best = d2 < d2best ? d2 : d2best;
+                    }
+                    cp = ccur;
+                    const float lc = fmaf(dx, c.y, -(dy * c.x));
+                    if (!((la > hi && lc > hi) || (la < lo && lc < lo))) {   // candidate segment j,
+                        const float s = ray_segment_time_filtered(a, c, qx, qy, dx, dy);   // ascending:
+                        if (s < best) { best = s; bi = j; }   // `s < best` keeps the first argmin
+                    }
+                    la = lc;
+                    a = c;
+                }
             }
         }
     };
+#endif
     const int nfull = (nv - 1) / kB * kB;   // segments in whole batches
     for (int j0 = 0; j0 < nfull; j0 += kB) batch(j0, BoolC<false>{});
     if (nfull < nv - 1) batch(nfull, BoolC<true>{});

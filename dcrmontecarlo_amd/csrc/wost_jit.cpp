@@ -410,6 +410,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
     if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
     if (exp_flags() & (1 << 29)) o << "#define WOST_EXP_UNIT_TAB 1\n";   // A/B: unit_direction's (n, y) table
+    if (exp_flags() & 131072) o << "#define WOST_EXP_SCAN_BITS 1\n";   // A/B: neumann_scan_both's per-vertex bits
     if ((exp_flags() >> 18) & 1023) o << "#define WOST_ABL_DUP " << ((exp_flags() >> 18) & 1023) << "\n";   // phase_dup.sh
     o << "#define WOST_JIT_TRIG_EXACT " << (exact_trig ? 1 : 0) << "\n";   // wost_set_trig
     if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";

@@ -25,7 +25,7 @@ REPO = os.path.dirname(HERE)
 def lib(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("scan") / "libscan_check.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
-                    "-I" + os.path.join(REPO, "include"), "-x", "hip", os.path.join(HERE, "native", "scan_check.cpp"),
+                    "-I" + os.path.join(REPO, "include"), *os.environ.get("WOST_SCAN_CHECK_DEFS", "").split(), "-x", "hip", os.path.join(HERE, "native", "scan_check.cpp"),
                     "-o", out], check=True)
     lb = ctypes.CDLL(out)
     fp = ctypes.POINTER(ctypes.c_float)
