@@ -1075,7 +1075,20 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         const int64_t want = (count + block - 1) / block;
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
         const int64_t waves = (int64_t)grid * (block / 64);
-        a.chunk = (int)std::max<int64_t>(1, std::min<int64_t>(1024, count / (waves * 4)));
+        // The work queue (wost_walk.h): every wave starts with a static chunk of up to 64
+        // walks (one per lane), then dequeues chunks of the rest from one global counter.
+        // All waves hitting the counter at the launch's start, and chunks of fewer than 64
+        // walks (several dequeues per refill), serialise on that one address: C2's 640k
+        // walks took 34k dequeues of 19 walks, 0.60 ms for 47 us of work
+        // (profiles/r05_ab/queue_chunk/).
+        int64_t chunk0 = std::min<int64_t>(64, (count + waves - 1) / waves);
+        if (const char* e = std::getenv("WOST_CHUNK0")) chunk0 = std::max(0, std::min(1024, std::atoi(e)));   // A/B
+        int64_t chunk_min = 64;
+        if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
+        a.chunk0 = (int32_t)chunk0;
+        a.queue_base = waves * chunk0;
+        const int64_t rest = count - std::min(count, a.queue_base);
+        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(1024, rest / (waves * 4)));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
         // on C4 and 10-14% slower on the short-walk scenarios: profiles/r02_ab/guided_queue.log)
         h->timing.grid_blocks = grid;

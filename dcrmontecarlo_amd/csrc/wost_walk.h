@@ -83,6 +83,11 @@ struct WalkArgs {
                                  // (0: each wave takes the class most of its walks are in)
     int32_t exact_trig;          // precompiled kernels: the direction's cos/sin correctly rounded
                                  // (wost_set_trig; the field-specialised kernels fix it at compile time)
+    // the work queue's static first fill: wave v of the grid starts with local walks
+    // [v * chunk0, (v + 1) * chunk0) (clamped to count) without touching the counter, and
+    // the counter's dequeues start at queue_base = waves * chunk0 (>= count: none)
+    int32_t chunk0;
+    int64_t queue_base;
 };
 
 // words of one parked walk: global id (2), local index (2), x, y, dD, step | onB << 31,
@@ -856,6 +861,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     // wave-uniform work-queue state
     uint64_t c_next = 0, c_end = 0;
     bool exhausted = false;
+    {   // the wave's static first chunk (no atomic at the launch's start, when every wave
+        // would hit the one counter at once)
+        const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        const uint64_t cnt = (uint64_t)A.count;
+        c_next = min(wv * (uint64_t)A.chunk0, cnt);
+        c_end = min(c_next + (uint64_t)A.chunk0, cnt);
+    }
 
     // per-lane walk state (solvers/WoStSolver.py:188-195)
     bool active = false;
@@ -980,8 +992,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         if (!kBatchEnd && __popcll(need) < WOST_REFILL_MIN && __any(active)) need = 0ull;
         while (need != 0ull && !exhausted) {
             if (c_next >= c_end) {
+                if (A.queue_base >= A.count) {   // the static chunks covered every walk
+                    exhausted = true;
+                    break;
+                }
                 unsigned long long c = 0;
                 if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)A.chunk);
+                c += (unsigned long long)A.queue_base;
                 // lane 0's value as a scalar (every lane runs the refill): the queue
                 // state stays in SGPRs and the refill loop's control flow uniform
                 c = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(c >> 32)) << 32) |
