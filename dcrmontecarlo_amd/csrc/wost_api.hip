@@ -230,6 +230,12 @@ struct wost_handle {
     int64_t point_alpha_cap = 0;
     uint32_t* d_pool = nullptr;       // walk pools of the tree kernels' workgroups (WalkArgs::pool)
     int64_t pool_cap = 0;
+    // pinned host staging of a solve's small copies (points, block ranges, block sums):
+    // a pageable hipMemcpyAsync costs ~9 us of host time each (profiles/r05_ab/host_path/)
+    char* h_pin = nullptr;
+    size_t pin_cap = 0;
+    bool counter_zero = false;        // d_counter is 0 (the block reduce resets it after each walk launch)
+    double last_steps_per_walk = 0.0; // the previous solve's mean steps per walk (the queue's chunk floor)
     wost_timing timing{};
 };
 
@@ -478,6 +484,19 @@ int ensure_cap(T*& p, int64_t& cap, int64_t need) {
     return WOST_OK;
 }
 
+// pinned host staging of at least `need` bytes (the stream is idle between solves)
+int ensure_pin(wost_handle* h, size_t need) {
+    if (need <= h->pin_cap) return WOST_OK;
+    if (h->h_pin) (void)hipHostFree(h->h_pin);
+    h->h_pin = nullptr;
+    h->pin_cap = 0;
+    need = std::max<size_t>(need, 4096);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&h->h_pin), need, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(WOST_ERR_OOM, "hipHostMalloc(%zu bytes): %s", need, hipGetErrorString(e));
+    h->pin_cap = need;
+    return WOST_OK;
+}
+
 // per-walk value and step buffers, always of equal capacity
 // Per-walk results of `need` walks with `ns` values each.
 int ensure_workspace(wost_handle* h, int64_t need, int ns = 1) {
@@ -540,6 +559,7 @@ void wost_destroy(wost_handle* h) {
                     h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree, h->d_seg_phi, h->d_point_alpha, h->d_pool};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (h->h_pin) (void)hipHostFree(h->h_pin);
     for (hipEvent_t& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -857,7 +877,17 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         return fail(WOST_ERR_INVALID_ARG, "walk range of %lld walks per point exceeds one launch (%lld walks)",
                     (long long)Wr, (long long)batch_limit);
     if ((rc = ensure_cap(h->d_points, h->points_cap, std::max<int64_t>(n_points, 1))) != WOST_OK) return rc;
-    HIP_TRY(hipMemcpyAsync(h->d_points, points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
+    // pinned staging: [points | one batch's block ranges | the block sums], 64-byte aligned
+    auto al64 = [](size_t b) { return (b + 63) / 64 * 64; };
+    const size_t pin_pts = al64(sizeof(float2) * (size_t)n_points);
+    const size_t pin_beg = al64(sizeof(int64_t) * (size_t)(nblk + 1));
+    const size_t pin_bs = al64(sizeof(double) * (size_t)(row * nblk));
+    if ((rc = ensure_pin(h, pin_pts + pin_beg + pin_bs)) != WOST_OK) return rc;
+    float* const pin_points = reinterpret_cast<float*>(h->h_pin);
+    int64_t* const pin_begin = reinterpret_cast<int64_t*>(h->h_pin + pin_pts);
+    double* const pin_bstats = reinterpret_cast<double*>(h->h_pin + pin_pts + pin_beg);
+    std::memcpy(pin_points, points, sizeof(float2) * (size_t)n_points);
+    HIP_TRY(hipMemcpyAsync(h->d_points, pin_points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
     if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, batch_limit), ns)) != WOST_OK) return rc;
     if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * row)) != WOST_OK) return rc;
     float* d_rec = nullptr;
@@ -1065,8 +1095,13 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         const int64_t nb = j2 - j;
 
         if ((rc = ensure_cap(h->d_begin, h->begin_cap, nb + 1)) != WOST_OK) return rc;
-        HIP_TRY(hipMemcpyAsync(h->d_begin, begins.data(), sizeof(int64_t) * (nb + 1), hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(hipMemsetAsync(h->d_counter, 0, sizeof(unsigned long long), h->stream));
+        // (the previous batch's copy from the staging has completed: its events were waited on)
+        std::memcpy(pin_begin, begins.data(), sizeof(int64_t) * (size_t)(nb + 1));
+        HIP_TRY(hipMemcpyAsync(h->d_begin, pin_begin, sizeof(int64_t) * (nb + 1), hipMemcpyHostToDevice, h->stream));
+        // the queue head: zeroed by the previous launch's block reduce, or here after a
+        // solve that stopped between a walk launch and its reduce
+        if (!h->counter_zero) HIP_TRY(hipMemsetAsync(h->d_counter, 0, sizeof(unsigned long long), h->stream));
+        h->counter_zero = false;
 
         a.out_val = h->d_val;
         a.out_steps = h->d_steps;
@@ -1083,12 +1118,18 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         // (profiles/r05_ab/queue_chunk/).
         int64_t chunk0 = std::min<int64_t>(64, (count + waves - 1) / waves);
         if (const char* e = std::getenv("WOST_CHUNK0")) chunk0 = std::max(0, std::min(1024, std::atoi(e)));   // A/B
-        int64_t chunk_min = 64;
+        // chunks below 64 walks (several dequeues per refill) pay when walks are short
+        // (C2: ~15 steps) and balance the launch's end when they are long (C5: ~208 steps):
+        // the floor is 1024 / (the handle's previous mean steps per walk), within [1, 64]
+        // (no previous solve: 64, or 1 for the tree kernels' long walks)
+        const double lp = h->last_steps_per_walk;
+        int64_t chunk_min = lp > 0.0 ? (int64_t)std::max(1.0, std::min(64.0, 1024.0 / lp)) : (mode_tree(mode) ? 1 : 64);
         if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
         a.chunk0 = (int32_t)chunk0;
         a.queue_base = waves * chunk0;
         const int64_t rest = count - std::min(count, a.queue_base);
-        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(1024, rest / (waves * 4)));
+        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(1024, (std::getenv("WOST_CHUNK_REST") ? rest : count) /
+                                                                              (waves * 4)));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
         // on C4 and 10-14% slower on the short-walk scenarios: profiles/r02_ab/guided_queue.log)
         h->timing.grid_blocks = grid;
@@ -1102,7 +1143,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         }
         HIP_TRY(hipEventRecord(h->ev[1], h->stream));
         HIP_TRY(launch_block_reduce(h->d_val, h->d_steps, h->d_begin, nb, ns, h->d_bstats + row * (j - block_begin),
-                                    h->stream));
+                                    h->d_counter, h->stream));
+        h->counter_zero = true;
         HIP_TRY(hipEventRecord(h->ev[2], h->stream));
         if (walk_values)
             HIP_TRY(hipMemcpyAsync(walk_values + walks_done * ns, h->d_val, sizeof(float) * count * ns,
@@ -1112,7 +1154,14 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         if (records)
             HIP_TRY(hipMemcpyAsync(records + walks_done * rec_stride * kRecFloats, d_rec, (size_t)count * rec_walk_bytes,
                                    hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipEventSynchronize(h->ev[2]));
+        const bool last = j2 >= block_end;
+        if (last) {   // the block sums ride the same wait
+            HIP_TRY(hipMemcpyAsync(pin_bstats, h->d_bstats, sizeof(double) * row * nblk, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipEventRecord(h->ev[5], h->stream));
+            HIP_TRY(hipEventSynchronize(h->ev[5]));
+        } else {
+            HIP_TRY(hipEventSynchronize(h->ev[2]));
+        }
         float t0 = 0.f, t1 = 0.f;
         HIP_TRY(hipEventElapsedTime(&t0, h->ev[0], h->ev[1]));
         HIP_TRY(hipEventElapsedTime(&t1, h->ev[1], h->ev[2]));
@@ -1134,10 +1183,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %.0f", c[i]);
         std::fprintf(stderr, "\n");
     }
-    std::vector<double> bs(row * nblk);
-    HIP_TRY(hipMemcpyAsync(bs.data(), h->d_bstats, sizeof(double) * row * nblk, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipEventRecord(h->ev[5], h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    const double* bs = pin_bstats;   // (copied and waited for with the last batch)
     float tt = 0.f;
     HIP_TRY(hipEventElapsedTime(&tt, h->ev[4], h->ev[5]));
 
@@ -1149,13 +1195,14 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
             for (int c = 0; c < row; ++c) point_stats[row * p + c] += bs[row * b + c];
         }
     }
-    if (block_stats) std::memcpy(block_stats, bs.data(), sizeof(double) * row * nblk);
+    if (block_stats) std::memcpy(block_stats, bs, sizeof(double) * row * nblk);
     h->timing.walk_kernel_ms = walk_ms;
     h->timing.reduce_kernel_ms = red_ms;
     h->timing.total_ms = tt;
     h->timing.n_launches = launches;
     h->timing.total_steps = steps_sum;
     h->timing.total_walks = (uint64_t)walks_total;
+    if (walks_total > 0) h->last_steps_per_walk = (double)steps_sum / (double)walks_total;
     h->timing.jit = jfn ? 1 : 0;
     h->timing.tree = mode_tree(mode) ? 1 : 0;
     return WOST_OK;

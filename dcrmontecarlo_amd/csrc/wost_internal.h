@@ -84,8 +84,10 @@ hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s);
 // Per-block reduction: block b covers local walks [begin[b], begin[b+1]).
 // ns values per walk (multi-source: val[walk * ns + k]); rows of 2*ns+1 doubles
 // (sum_k, sumsq_k for each k, then steps).
+// counter_reset (may be null): the walk queue's head, set to 0 for the next walk launch
 hipError_t launch_block_reduce(const float* val, const uint32_t* steps, const int64_t* begin,
-                               int64_t nblocks, int ns, double* out, hipStream_t s);
+                               int64_t nblocks, int ns, double* out, unsigned long long* counter_reset,
+                               hipStream_t s);
 
 hipError_t launch_geometry_query(int op, const float2* verts, int nv, const float2* pts,
                                  const float2* dirs, const float* radii, int64_t n,

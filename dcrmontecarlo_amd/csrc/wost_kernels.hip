@@ -206,9 +206,11 @@ constexpr int kReduceBlock = 256;
 // the same for every ns, so source k's sums do not depend on the other sources.
 __global__ void __launch_bounds__(kReduceBlock)
 wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ steps,
-                  const int64_t* __restrict__ begin, int64_t nblocks, int ns, double* __restrict__ out) {
+                  const int64_t* __restrict__ begin, int64_t nblocks, int ns, double* __restrict__ out,
+                  unsigned long long* counter_reset) {
     __shared__ double s_sum[kReduceBlock], s_sq[kReduceBlock], s_st[kReduceBlock];
     const int row = 2 * ns + 1;
+    if (counter_reset != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *counter_reset = 0ull;   // (a vector store)
     for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
         const int64_t lo = begin[b], hi = begin[b + 1];
         for (int k = 0; k < ns; ++k) {
@@ -243,10 +245,12 @@ wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ st
 }
 
 hipError_t launch_block_reduce(const float* val, const uint32_t* steps, const int64_t* begin,
-                               int64_t nblocks, int ns, double* out, hipStream_t s) {
-    if (nblocks <= 0) return hipSuccess;
+                               int64_t nblocks, int ns, double* out, unsigned long long* counter_reset,
+                               hipStream_t s) {
+    if (nblocks <= 0) return counter_reset ? hipMemsetAsync(counter_reset, 0, sizeof(unsigned long long), s)
+                                           : hipSuccess;
     const int grid = (int)(nblocks < 65536 ? nblocks : 65536);
-    wost_block_reduce<<<grid, kReduceBlock, 0, s>>>(val, steps, begin, nblocks, ns, out);
+    wost_block_reduce<<<grid, kReduceBlock, 0, s>>>(val, steps, begin, nblocks, ns, out, counter_reset);
     return hipGetLastError();
 }
 
