@@ -1106,7 +1106,10 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.out_val = h->d_val;
         a.out_steps = h->d_steps;
         a.count = count;
-        const int64_t max_grid = (int64_t)blocks_per_cu * h->num_cus;
+        int64_t bpc = blocks_per_cu;
+        if (const char* e = std::getenv("WOST_GRID_BLOCKS_PER_CU"))   // A/B: fewer resident workgroups
+            bpc = std::max<int64_t>(1, std::min<int64_t>(bpc, std::atoi(e)));
+        const int64_t max_grid = bpc * h->num_cus;
         const int64_t want = (count + block - 1) / block;
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
         const int64_t waves = (int64_t)grid * (block / 64);
@@ -1121,9 +1124,10 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         // chunks below 64 walks (several dequeues per refill) pay when walks are short
         // (C2: ~15 steps) and balance the launch's end when they are long (C5: ~208 steps):
         // the floor is 1024 / (the handle's previous mean steps per walk), within [1, 64]
-        // (no previous solve: 64, or 1 for the tree kernels' long walks)
+        // (no previous solve: 64 for Dirichlet-only problems, whose walks are short, and 1
+        // with a Neumann boundary: C4, the DCR notebook and C5 walk 76-208 steps)
         const double lp = h->last_steps_per_walk;
-        int64_t chunk_min = lp > 0.0 ? (int64_t)std::max(1.0, std::min(64.0, 1024.0 / lp)) : (mode_tree(mode) ? 1 : 64);
+        int64_t chunk_min = lp > 0.0 ? (int64_t)std::max(1.0, std::min(64.0, 1024.0 / lp)) : (mode_neu(mode) ? 1 : 64);
         if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
         a.chunk0 = (int32_t)chunk0;
         a.queue_base = waves * chunk0;
