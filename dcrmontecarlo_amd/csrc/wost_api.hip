@@ -1107,8 +1107,16 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.out_steps = h->d_steps;
         a.count = count;
         int64_t bpc = blocks_per_cu;
+        // short walks (the handle's previous solve: < 32 steps per walk) and few of them per
+        // lane (C2: 640k walks, ~1.2 per lane at full occupancy): the launch lasts as long as
+        // its longest walk chains, whose steps run faster with fewer waves per SIMD, so
+        // fewer resident workgroups, ~4 walks per lane and at least 2 workgroups per CU
+        // (C2: 0.21 -> 0.18 ms per launch, profiles/r05_ab/grid_c2/)
+        const double lw = h->last_steps_per_walk;
+        if (lw > 0.0 && lw < 32.0 && bpc > 2)
+            bpc = std::max<int64_t>(2, std::min<int64_t>(bpc, count / ((int64_t)h->num_cus * block * 4)));
         if (const char* e = std::getenv("WOST_GRID_BLOCKS_PER_CU"))   // A/B: fewer resident workgroups
-            bpc = std::max<int64_t>(1, std::min<int64_t>(bpc, std::atoi(e)));
+            bpc = std::max<int64_t>(1, std::min<int64_t>((int64_t)blocks_per_cu, std::atoi(e)));
         const int64_t max_grid = bpc * h->num_cus;
         const int64_t want = (count + block - 1) / block;
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
@@ -1119,7 +1127,13 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         // walks (several dequeues per refill), serialise on that one address: C2's 640k
         // walks took 34k dequeues of 19 walks, 0.60 ms for 47 us of work
         // (profiles/r05_ab/queue_chunk/).
-        int64_t chunk0 = std::min<int64_t>(64, (count + waves - 1) / waves);
+        // The static chunks serve short walks (C2). Long walks lose by them when launches
+        // run concurrently (the C5 survey's handle pairs: a late-starting wave still owns its
+        // 64 walks; 1.38e10 -> 1.34e10, profiles/r05_ab/queue_c5/): only after a solve of
+        // < 32 steps per walk, or, with no previous solve, without a Neumann boundary.
+        const double ls = h->last_steps_per_walk;
+        const bool short_walks = ls > 0.0 ? ls < 32.0 : !mode_neu(mode);
+        int64_t chunk0 = short_walks ? std::min<int64_t>(64, (count + waves - 1) / waves) : 0;
         if (const char* e = std::getenv("WOST_CHUNK0")) chunk0 = std::max(0, std::min(1024, std::atoi(e)));   // A/B
         // chunks below 64 walks (several dequeues per refill) pay when walks are short
         // (C2: ~15 steps) and balance the launch's end when they are long (C5: ~208 steps):
