@@ -1106,14 +1106,17 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.out_val = h->d_val;
         a.out_steps = h->d_steps;
         a.count = count;
+        // The launch's shape from the handle's previous solve (its mean steps per walk; 0:
+        // none). Short walks (< 32 steps; with no previous solve: no Neumann boundary) are
+        // cheap enough that the queue's shared counter and the launch's tail set the time.
+        const double prev_steps = h->last_steps_per_walk;
+        const bool short_walks = prev_steps > 0.0 ? prev_steps < 32.0 : !mode_neu(mode);
+        // Resident workgroups: after a solve of short walks, few of them per lane (C2: 640k
+        // walks, ~1.2 per lane at full occupancy) leave the launch as long as its longest
+        // walk chains, whose steps run faster with fewer waves per SIMD: ~4 walks per lane,
+        // at least 2 workgroups per CU (C2: 0.21 -> 0.18 ms per launch, profiles/r05_ab/grid_c2/)
         int64_t bpc = blocks_per_cu;
-        // short walks (the handle's previous solve: < 32 steps per walk) and few of them per
-        // lane (C2: 640k walks, ~1.2 per lane at full occupancy): the launch lasts as long as
-        // its longest walk chains, whose steps run faster with fewer waves per SIMD, so
-        // fewer resident workgroups, ~4 walks per lane and at least 2 workgroups per CU
-        // (C2: 0.21 -> 0.18 ms per launch, profiles/r05_ab/grid_c2/)
-        const double lw = h->last_steps_per_walk;
-        if (lw > 0.0 && lw < 32.0 && bpc > 2)
+        if (prev_steps > 0.0 && short_walks && bpc > 2)
             bpc = std::max<int64_t>(2, std::min<int64_t>(bpc, count / ((int64_t)h->num_cus * block * 4)));
         if (const char* e = std::getenv("WOST_GRID_BLOCKS_PER_CU"))   // A/B: fewer resident workgroups
             bpc = std::max<int64_t>(1, std::min<int64_t>((int64_t)blocks_per_cu, std::atoi(e)));
@@ -1121,33 +1124,26 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         const int64_t want = (count + block - 1) / block;
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
         const int64_t waves = (int64_t)grid * (block / 64);
-        // The work queue (wost_walk.h): every wave starts with a static chunk of up to 64
-        // walks (one per lane), then dequeues chunks of the rest from one global counter.
-        // All waves hitting the counter at the launch's start, and chunks of fewer than 64
-        // walks (several dequeues per refill), serialise on that one address: C2's 640k
-        // walks took 34k dequeues of 19 walks, 0.60 ms for 47 us of work
-        // (profiles/r05_ab/queue_chunk/).
-        // The static chunks serve short walks (C2). Long walks lose by them when launches
-        // run concurrently (the C5 survey's handle pairs: a late-starting wave still owns its
-        // 64 walks; 1.38e10 -> 1.34e10, profiles/r05_ab/queue_c5/): only after a solve of
-        // < 32 steps per walk, or, with no previous solve, without a Neumann boundary.
-        const double ls = h->last_steps_per_walk;
-        const bool short_walks = ls > 0.0 ? ls < 32.0 : !mode_neu(mode);
+        // The work queue (wost_walk.h): static chunks of up to 64 walks per wave (one per
+        // lane), then chunks of the rest from one global counter. Every dequeue of that
+        // counter serialises at its address (~11-16 ns): C2's 640k walks took 34k dequeues of
+        // 19 walks, all waves hitting the counter at the launch's start, 0.60 ms for 47 us of
+        // work (profiles/r05_ab/queue_chunk/, queue_static/).
+        // - static chunks for short walks only: long walks lose by them when launches run
+        //   concurrently (the C5 survey's handle pairs: a late-starting wave still owns its 64
+        //   walks; 1.38e10 -> 1.34e10, profiles/r05_ab/queue_c5/);
+        // - the dynamic chunk's floor: 1024 / (previous mean steps per walk) within [1, 64]
+        //   (no previous solve: 64, or 1 with a Neumann boundary, whose walks -- C4, the DCR
+        //   notebook, C5 -- run 76-208 steps): chunks below 64 walks (several dequeues per
+        //   refill) cost short walks the counter's time and balance long walks' launch ends.
         int64_t chunk0 = short_walks ? std::min<int64_t>(64, (count + waves - 1) / waves) : 0;
         if (const char* e = std::getenv("WOST_CHUNK0")) chunk0 = std::max(0, std::min(1024, std::atoi(e)));   // A/B
-        // chunks below 64 walks (several dequeues per refill) pay when walks are short
-        // (C2: ~15 steps) and balance the launch's end when they are long (C5: ~208 steps):
-        // the floor is 1024 / (the handle's previous mean steps per walk), within [1, 64]
-        // (no previous solve: 64 for Dirichlet-only problems, whose walks are short, and 1
-        // with a Neumann boundary: C4, the DCR notebook and C5 walk 76-208 steps)
-        const double lp = h->last_steps_per_walk;
-        int64_t chunk_min = lp > 0.0 ? (int64_t)std::max(1.0, std::min(64.0, 1024.0 / lp)) : (mode_neu(mode) ? 1 : 64);
+        int64_t chunk_min = prev_steps > 0.0 ? (int64_t)std::max(1.0, std::min(64.0, 1024.0 / prev_steps))
+                                             : (mode_neu(mode) ? 1 : 64);
         if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
         a.chunk0 = (int32_t)chunk0;
         a.queue_base = waves * chunk0;
-        const int64_t rest = count - std::min(count, a.queue_base);
-        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(1024, (std::getenv("WOST_CHUNK_REST") ? rest : count) /
-                                                                              (waves * 4)));
+        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(1024, count / (waves * 4)));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
         // on C4 and 10-14% slower on the short-walk scenarios: profiles/r02_ab/guided_queue.log)
         h->timing.grid_blocks = grid;
