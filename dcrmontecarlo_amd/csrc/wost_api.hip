@@ -484,10 +484,13 @@ int ensure_cap(T*& p, int64_t& cap, int64_t need) {
     return WOST_OK;
 }
 
-// pinned host staging of at least `need` bytes (the stream is idle between solves)
+// pinned host staging of at least `need` bytes
 int ensure_pin(wost_handle* h, size_t need) {
     if (need <= h->pin_cap) return WOST_OK;
-    if (h->h_pin) (void)hipHostFree(h->h_pin);
+    if (h->h_pin) {   // (a solve that failed mid-way may have left copies from it queued)
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipHostFree(h->h_pin);
+    }
     h->h_pin = nullptr;
     h->pin_cap = 0;
     need = std::max<size_t>(need, 4096);
@@ -1143,7 +1146,9 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
         a.chunk0 = (int32_t)chunk0;
         a.queue_base = waves * chunk0;
-        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(1024, count / (waves * 4)));
+        int64_t chunk_max = 1024;
+        if (const char* e = std::getenv("WOST_CHUNK_MAX")) chunk_max = std::max(1, std::min(1 << 20, std::atoi(e)));   // A/B
+        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(chunk_max, count / (waves * 4)));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
         // on C4 and 10-14% slower on the short-walk scenarios: profiles/r02_ab/guided_queue.log)
         h->timing.grid_blocks = grid;
