@@ -1146,7 +1146,10 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
         a.chunk0 = (int32_t)chunk0;
         a.queue_base = waves * chunk0;
-        int64_t chunk_max = 1024;
+        // the cap: a wave's last chunk is work no other wave can take when the queue runs out;
+        // 64 walks (one per lane) instead of 1,024: C4 1.26e11 -> 1.31e11, C3 4.74e10 ->
+        // 5.20e10 walk-steps/s (profiles/r05_ab/chunk_cap/)
+        int64_t chunk_max = 64;
         if (const char* e = std::getenv("WOST_CHUNK_MAX")) chunk_max = std::max(1, std::min(1 << 20, std::atoi(e)));   // A/B
         a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(chunk_max, count / (waves * 4)));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
