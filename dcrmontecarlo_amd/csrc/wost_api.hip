@@ -1148,8 +1148,9 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.queue_base = waves * chunk0;
         // the cap: a wave's last chunk is work no other wave can take when the queue runs out;
         // 64 walks (one per lane) instead of 1,024: C4 1.26e11 -> 1.31e11, C3 4.74e10 ->
-        // 5.20e10 walk-steps/s (profiles/r05_ab/chunk_cap/)
-        int64_t chunk_max = 64;
+        // 5.20e10 walk-steps/s; after walks of >= 128 steps 16 (their dequeues are rare):
+        // the C5 survey 1.42e10 -> 1.46e10 (profiles/r05_ab/chunk_cap/)
+        int64_t chunk_max = prev_steps >= 128.0 ? 16 : 64;
         if (const char* e = std::getenv("WOST_CHUNK_MAX")) chunk_max = std::max(1, std::min(1 << 20, std::atoi(e)));   // A/B
         a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(chunk_max, count / (waves * 4)));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
