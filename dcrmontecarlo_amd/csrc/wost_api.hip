@@ -236,6 +236,7 @@ struct wost_handle {
     size_t pin_cap = 0;
     bool counter_zero = false;        // d_counter is 0 (the block reduce resets it after each walk launch)
     double last_steps_per_walk = 0.0; // the previous solve's mean steps per walk (the queue's chunk floor)
+    double last_steps_per_s = 0.0;    // ... and its walk kernels' walk-steps per second
     wost_timing timing{};
 };
 
@@ -1143,6 +1144,13 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         if (const char* e = std::getenv("WOST_CHUNK0")) chunk0 = std::max(0, std::min(1024, std::atoi(e)));   // A/B
         int64_t chunk_min = prev_steps > 0.0 ? (int64_t)std::max(1.0, std::min(64.0, 1024.0 / prev_steps))
                                              : (mode_neu(mode) ? 1 : 64);
+        // and at most ~40M dequeues per second at the previous solve's rate: cheap short walks
+        // (Laplace, Poisson: ~2e11 walk-steps/s at ~14 steps per walk) need chunks of
+        // several hundred walks, or the counter sets the pace (64-walk chunks: 2.1e11 ->
+        // 7.0e10 walk-steps/s, profiles/r05_ab/chunk_cap/scenarios_cap64.log)
+        if (prev_steps > 0.0 && h->last_steps_per_s > 0.0)
+            chunk_min = std::max<int64_t>(chunk_min, std::min<int64_t>(1024, (int64_t)std::ceil(
+                                                         h->last_steps_per_s / (prev_steps * 4.0e7))));
         if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
         a.chunk0 = (int32_t)chunk0;
         a.queue_base = waves * chunk0;
@@ -1226,6 +1234,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     h->timing.total_steps = steps_sum;
     h->timing.total_walks = (uint64_t)walks_total;
     if (walks_total > 0) h->last_steps_per_walk = (double)steps_sum / (double)walks_total;
+    h->last_steps_per_s = walk_ms > 0.0 ? (double)steps_sum / (walk_ms * 1e-3) : 0.0;
     h->timing.jit = jfn ? 1 : 0;
     h->timing.tree = mode_tree(mode) ? 1 : 0;
     return WOST_OK;
