@@ -22,7 +22,7 @@ WOST_ERR_UNSUPPORTED = -4
 WOST_ERR_OOM = -5
 WOST_ERR_COMM = -6
 
-ABI_VERSION = 4   # include/wost.h WOST_ABI_VERSION
+ABI_VERSION = 5   # include/wost.h WOST_ABI_VERSION
 WOST_COMM_ID_BYTES = 128
 WOST_COMM_SUM, WOST_COMM_MAX = 0, 1
 WOST_BLOCK_WALKS = 4096
@@ -64,7 +64,11 @@ class WostProblem(ctypes.Structure):
 class WostTiming(ctypes.Structure):
     _fields_ = [("walk_kernel_ms", c_double), ("reduce_kernel_ms", c_double), ("total_ms", c_double),
                 ("n_launches", c_int32), ("grid_blocks", c_int32), ("total_steps", c_uint64),
-                ("total_walks", c_uint64), ("jit", c_int32), ("tree", c_int32)]
+                ("total_walks", c_uint64), ("jit", c_int32), ("tree", c_int32),
+                ("blocks_per_cu", c_int32), ("block_threads", c_int32), ("chunk0", c_int32), ("chunk", c_int32),
+                ("adaptive", c_int32), ("max_walk_steps", c_uint32), ("jit_ms", c_double), ("span_ms", c_double),
+                ("tail_ms", c_double), ("last_wave_ms", c_double), ("last_wave_iters", c_uint32),
+                ("max_wave_iters", c_uint32)]
 
 
 class WostDistTiming(ctypes.Structure):
@@ -146,6 +150,9 @@ def _load():
         "wost_set_trig": (c_int32, [H, c_int32]),
         "wost_set_fixed_step_check": (c_int32, [H, c_int32]),
         "wost_set_segment_tree": (c_int32, [H, c_int32, c_int32]),
+        "wost_set_option": (c_int32, [H, c_char_p, c_double]),
+        "wost_get_option": (c_int32, [H, c_char_p, POINTER(c_double)]),
+        "wost_options_report": (c_int32, [H, ctypes.c_char_p, c_int64, POINTER(c_int64)]),
         "wost_kernel_source": (c_int32, [POINTER(WostProblem), ctypes.c_char_p, c_int64, POINTER(c_int64)]),
         "wost_eval_field": (c_int32, [H, c_int32, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_sampler_table": (c_int32, [H, POINTER(c_float), c_int32]),
@@ -178,6 +185,18 @@ def check(rc: int, what: str = "libwost", comm: bool = False):
     if rc == WOST_ERR_UNSUPPORTED:
         raise NotImplementedError(f"{what}: {msg}")
     raise WostError(f"{what} failed ({rc}): {msg}")
+
+
+def options_report(h=None) -> dict:
+    """wost_options_report: {"build": "product"|"study", "non_default": {...}} of a handle
+    (None: the library's build only)."""
+    import json
+
+    n = c_int64(0)
+    check(lib.wost_options_report(h, None, 0, ctypes.byref(n)), "wost_options_report")
+    buf = ctypes.create_string_buffer(n.value + 1)
+    check(lib.wost_options_report(h, buf, n.value + 1, ctypes.byref(n)), "wost_options_report")
+    return json.loads(buf.value.decode())
 
 
 def device_count() -> int:

@@ -17,6 +17,7 @@
 #include "wost_device.h"
 #include "wost_internal.h"
 #include "wost_jit.h"
+#include "wost_options.h"
 #include "wost_tables.h"
 #include "wost_tree.h"
 
@@ -192,6 +193,9 @@ struct wost_handle {
     bool fixed_step_check = true;
     int trig_mode = WOST_TRIG_AUTO;       // wost_set_trig
 
+    // kernel and launch options (wost_set_option; study builds: also the A/B environment)
+    Options opt;
+
     // field-specialised walk kernel (wost_jit.cpp)
     bool jit_enabled = true;
     hipFunction_t jit_fn = nullptr;
@@ -216,7 +220,8 @@ struct wost_handle {
     float* d_table = nullptr;
     char* d_prog = nullptr;
     size_t d_prog_cap = 0;
-    unsigned long long* d_counter = nullptr;
+    unsigned long long* d_counter = nullptr;   // the walk launches' control words (wost_walk.h kCtlWords)
+    int64_t ctl_cap = 0;                       // ... words allocated
     float* d_val = nullptr;
     uint32_t* d_steps = nullptr;
     int64_t ws_cap = 0, ws_val_cap = 0;
@@ -230,13 +235,12 @@ struct wost_handle {
     int64_t point_alpha_cap = 0;
     uint32_t* d_pool = nullptr;       // walk pools of the tree kernels' workgroups (WalkArgs::pool)
     int64_t pool_cap = 0;
+    double tick_khz = 100000.0;       // the device wall clock (hipDeviceAttributeWallClockRate)
     // pinned host staging of a solve's small copies (points, block ranges, block sums):
     // a pageable hipMemcpyAsync costs ~9 us of host time each (profiles/r05_ab/host_path/)
     char* h_pin = nullptr;
     size_t pin_cap = 0;
     bool counter_zero = false;        // d_counter is 0 (the block reduce resets it after each walk launch)
-    double last_steps_per_walk = 0.0; // the previous solve's mean steps per walk (the queue's chunk floor)
-    double last_steps_per_s = 0.0;    // ... and its walk kernels' walk-steps per second
     wost_timing timing{};
 };
 
@@ -249,12 +253,9 @@ constexpr int64_t kMaxBatchWalks = int64_t(1) << 26;   // 64 Mi walks = 512 MiB 
 // polylines under compat="fixed" (which scans them), work at any length.
 constexpr size_t kGlobalPolylineLdsBytes = 40 * 1024;
 
-// study builds: WOST_TREE_ITER_STATS=1 compiles the tree queries' loop counters into the
-// field-specialised kernels (wost_walk.h) and prints their sums after each solve
-bool tree_iter_stats() {
-    const char* e = std::getenv("WOST_TREE_ITER_STATS");
-    return e && std::atoi(e) == 1;
-}
+// The solve's launch statistics (the walk kernel's per-wave records, wost_block_reduce)
+// ride in front of the block sums in d_bstats, so that one copy brings both to the host.
+constexpr int64_t kLstatsWords = 8;
 
 int upload_program(wost_handle* h) {
     if (!h->prog_dirty) return WOST_OK;
@@ -283,7 +284,7 @@ bool exact_trig_of(const wost_handle* h) {
 }
 
 hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock,
-                         bool global_polylines = false, int tree_stage = 0) {
+                         bool global_polylines = false, int tree_stage = 0, double* compile_ms = nullptr) {
     if (!h->jit_enabled) return nullptr;
     // the cache key holds everything the source depends on: the staging level, the
     // exact workgroup size (a multiple of 64, at most 1024) and the trig choice
@@ -297,18 +298,22 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
     h->jit_version = h->prog_version;
     const int nn = (int)(h->nverts.size() / 2);
     std::vector<float> phi;   // a compiled-in Neumann polyline carries the device's segment angles
-    if (jit_const_neumann(mode, nn) && nn >= 2) {
+    if (jit_const_neumann(h->opt, mode, nn) && nn >= 2) {
         phi.resize(nn - 1);
         if (hipMemcpy(phi.data(), h->d_seg_phi, sizeof(float) * phi.size(), hipMemcpyDeviceToHost) != hipSuccess)
             return nullptr;
     }
-    const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
-                                         (int)(h->dverts.size() / 2), h->nverts.data(), nn, record, ns, block,
-                                         phi.empty() ? nullptr : phi.data(), global_polylines, tree_stage, exact);
+    const std::string src = jit_generate(h->opt, mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(),
+                                         h->dverts.data(), (int)(h->dverts.size() / 2), h->nverts.data(), nn, record,
+                                         ns, block, phi.empty() ? nullptr : phi.data(), global_polylines, tree_stage,
+                                         exact);
     std::string err;
     hipFunction_t fn = nullptr;
     hipFunction_t afn = nullptr;
-    if (!jit_get_kernel(h->device, src, &fn, &err, &afn)) {
+    double cms = 0.0;
+    const bool ok = jit_get_kernel(h->opt, h->device, src, &fn, &err, &afn, &cms);
+    if (compile_ms) *compile_ms += cms;
+    if (!ok) {
         h->jit_error = err;
         std::fprintf(stderr, "libwost: field-specialised kernel unavailable, using the precompiled one: %s\n",
                      err.c_str());
@@ -412,8 +417,8 @@ float silhouette_stop2(float rmin) {
 // What of the segment tree the field-specialised kernels stage in LDS, by level:
 // 2 = its records and the Neumann vertices (one kTreeStageVertsBlock-thread workgroup
 // per CU), 1 = its records (two kTreeStageBlock-thread workgroups per CU), 0 = nothing
-// (256-thread workgroups, records and vertices through L1/L2). WOST_TREE_LDS caps the
-// level (A/B; the results are the same bits at every level). Returns the records to
+// (256-thread workgroups, records and vertices through L1/L2). The option tree_lds caps
+// the level (A/B; the results are the same bits at every level). Returns the records to
 // stage and sets the workgroup size and the vertices to stage.
 constexpr size_t kTreeLdsMaxBytes = 64 * 1024;
 constexpr int kTreeLdsDefaultLevel = 2;
@@ -421,7 +426,7 @@ int tree_lds_records(const wost_handle* h, int mode, int level, int* block, int*
     *block = kWalkBlock;
     *verts = 0;
     if (!mode_tree(mode) || !h->tree_ready) return 0;
-    if (const char* e = std::getenv("WOST_TREE_LDS")) level = std::min(level, std::max(0, std::atoi(e)));
+    level = std::min(level, h->opt.tree_lds);
     const int n = h->tree.first_leaf;
     if (level <= 0 || n <= 0 || (size_t)n * 8 * sizeof(float4) > kTreeLdsMaxBytes) return 0;
     if (level >= 2) {
@@ -429,9 +434,7 @@ int tree_lds_records(const wost_handle* h, int mode, int level, int* block, int*
         *verts = (int)(h->nverts.size() / 2);
         return n;
     }
-    int b = kTreeStageBlock;
-    if (const char* e = std::getenv("WOST_TREE_LDS_BLOCK")) b = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
-    *block = b;
+    *block = h->opt.tree_lds_block;
     return n;
 }
 
@@ -593,12 +596,17 @@ int create_host(const wost_problem* pb, wost_handle** out) {
         return rc;
     }
     h->compat = pb->compat;
+#if defined(WOST_STUDY)
+    // study builds only: the tools' A/B environment (the product library reads none of it;
+    // wost_set_jit / wost_set_trig / wost_set_segment_tree / wost_set_option instead)
     if (const char* e = std::getenv("WOST_JIT")) h->jit_enabled = std::strcmp(e, "0") != 0;
     if (const char* e = std::getenv("WOST_TREE_MIN_SEGMENTS")) h->tree_min_segments = std::atoi(e);
     if (const char* e = std::getenv("WOST_TRIG"))
         h->trig_mode = std::strcmp(e, "exact") == 0 ? WOST_TRIG_EXACT : std::strcmp(e, "fast") == 0 ? WOST_TRIG_FAST
                                                                                                    : WOST_TRIG_AUTO;
     if (const char* e = std::getenv("WOST_TREE_LEAF")) h->tree_leaf = std::min(32, std::max(1, std::atoi(e)));
+#endif
+    options_from_study_env(h->opt);
     // solvers/WoStSolver.py:54-64: any of sigma/alpha turns on delta tracking,
     // the missing one defaults to sigma = 0 / alpha = 1 (constant => Q9 fallback).
     h->delta = h->fields[SLOT_SIGMA].present || h->fields[SLOT_ALPHA].present;
@@ -664,9 +672,16 @@ int wost_create(const wost_problem* pb, wost_handle** out) {
     } while (0)
     CREATE_TRY(hipSetDevice(h->device));
     CREATE_TRY(hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, h->device));
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) == hipSuccess && khz > 0)
+            h->tick_khz = (double)khz;
+    }
     CREATE_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     for (hipEvent_t& ev : h->ev) CREATE_TRY(hipEventCreate(&ev));
-    CREATE_TRY(hipMalloc(&h->d_counter, sizeof(unsigned long long)));
+    h->ctl_cap = (int64_t)ctl_words(8192);   // 8,192 waves: 256 CUs x 32
+    CREATE_TRY(hipMalloc(&h->d_counter, sizeof(unsigned long long) * (size_t)h->ctl_cap));
+    CREATE_TRY(hipMemset(h->d_counter, 0, sizeof(unsigned long long) * (size_t)h->ctl_cap));
     CREATE_TRY(hipMalloc(&h->d_dverts, sizeof(float) * h->dverts.size()));
     CREATE_TRY(hipMemcpy(h->d_dverts, h->dverts.data(), sizeof(float) * h->dverts.size(), hipMemcpyHostToDevice));
     if (!h->nverts.empty()) {
@@ -885,7 +900,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     auto al64 = [](size_t b) { return (b + 63) / 64 * 64; };
     const size_t pin_pts = al64(sizeof(float2) * (size_t)n_points);
     const size_t pin_beg = al64(sizeof(int64_t) * (size_t)(nblk + 1));
-    const size_t pin_bs = al64(sizeof(double) * (size_t)(row * nblk));
+    const size_t pin_bs = al64(sizeof(double) * (size_t)(kLstatsWords + row * nblk));
     if ((rc = ensure_pin(h, pin_pts + pin_beg + pin_bs)) != WOST_OK) return rc;
     float* const pin_points = reinterpret_cast<float*>(h->h_pin);
     int64_t* const pin_begin = reinterpret_cast<int64_t*>(h->h_pin + pin_pts);
@@ -893,7 +908,10 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     std::memcpy(pin_points, points, sizeof(float2) * (size_t)n_points);
     HIP_TRY(hipMemcpyAsync(h->d_points, pin_points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
     if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, batch_limit), ns)) != WOST_OK) return rc;
-    if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, nblk * row)) != WOST_OK) return rc;
+    if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, kLstatsWords + nblk * row)) != WOST_OK) return rc;
+    // (the launch statistics in front of the block sums: one copy brings both)
+    unsigned long long* const d_lstats = reinterpret_cast<unsigned long long*>(h->d_bstats);
+    double* const d_rows = h->d_bstats + kLstatsWords;
     float* d_rec = nullptr;
     struct RecFree {
         float*& p;
@@ -904,31 +922,33 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     int block = kWalkBlock, tree_verts = 0;
     int tree_level = kTreeLdsDefaultLevel;
     int tree_lds = h->jit_enabled ? tree_lds_records(h, mode, tree_level, &block, &tree_verts) : 0;
-    // A/B knob: the workgroup of the field-specialised scan kernels (WOST_WALK_BLOCK, a multiple
-    // of 64 up to 1024): larger workgroups share one LDS copy of the sampler and G_norm tables,
+    // option walk_block: the workgroup of the field-specialised scan kernels (a multiple of
+    // 64 up to 1024): larger workgroups share one LDS copy of the sampler and G_norm tables,
     // so more waves fit a CU than 256-thread workgroups allow (results are the same bits)
-    if (h->jit_enabled && !mode_tree(mode))
-        if (const char* e = std::getenv("WOST_WALK_BLOCK")) block = std::max(64, std::min(1024, std::atoi(e) / 64 * 64));
+    if (h->jit_enabled && !mode_tree(mode) && h->opt.walk_block > 0) block = h->opt.walk_block;
     const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
+    const Options& O = h->opt;
+    double jit_ms = 0.0;
     // polylines whose LDS copy would cost the walk kernel its occupancy are read from
     // global memory instead (field-specialised kernels; the precompiled ones stage them)
     // (the staged tree records have their own budget, kTreeLdsMaxBytes)
     bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0,
-                                                  jit_const_dirichlet(nd_)) > kGlobalPolylineLdsBytes;
+                                                  jit_const_dirichlet(O, nd_)) > kGlobalPolylineLdsBytes;
     // the brute-force scan of a long Neumann polyline (neumann_scan_both) reads every vertex
     // at every step: staged in LDS with one 1024-thread workgroup per CU when it fits (a
     // broadcast LDS read per vertex), else from global memory
-    if (gpoly && h->jit_enabled && jit_fused_neumann_scan(mode, nn_)) {
+    if (gpoly && h->jit_enabled && jit_fused_neumann_scan(O, mode, nn_)) {
         int cap = 0;
         HIP_TRY(hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device));
-        if (walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0, jit_const_dirichlet(nd_), false, false,
+        if (walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0, jit_const_dirichlet(O, nd_), false, false,
                            kTreeStageVertsBlock) <= (size_t)cap) {
             gpoly = false;
             block = kTreeStageVertsBlock;
         }
     }
     auto stage_of = [](int recs, int verts) { return recs > 0 ? (verts > 0 ? 2 : 1) : 0; };
-    hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts));
+    hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts),
+                                   &jit_ms);
     if (!jfn && block != kWalkBlock) {   // the precompiled kernels run 256-thread workgroups, no staged tree
         block = kWalkBlock;
         tree_lds = 0;
@@ -936,11 +956,11 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     }
     if (ns > 1 && !jfn)
         return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel%s%s",
-                    h->jit_enabled ? ": " : " (disabled by wost_set_jit / WOST_JIT=0)", h->jit_error.c_str());
-    size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(nd_),
-                                jfn && jit_const_neumann(mode, nn_), jfn && gpoly, block, tree_verts);
-    // A/B knob (occupancy studies): WOST_LDS_PAD_BYTES extra bytes of LDS per workgroup
-    if (const char* e = std::getenv("WOST_LDS_PAD_BYTES")) lds += (size_t)std::max(0, std::atoi(e));
+                    h->jit_enabled ? ": " : " (disabled by wost_set_jit)", h->jit_error.c_str());
+    size_t lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jfn && jit_const_dirichlet(O, nd_),
+                                jfn && jit_const_neumann(O, mode, nn_), jfn && gpoly, block, tree_verts);
+    // option lds_pad_bytes (occupancy studies): extra bytes of LDS per workgroup
+    lds += (size_t)O.lds_pad_bytes;
     int blocks_per_cu = 0;
     // a workgroup whose LDS exceeds the CU's never fits: checked here, not left to the
     // occupancy query
@@ -958,7 +978,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         // from 256-thread workgroups
         tree_level = tree_verts > 0 ? 1 : 0;
         tree_lds = tree_lds_records(h, mode, tree_level, &block, &tree_verts);
-        if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts)))) {
+        if (!(jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts),
+                               &jit_ms))) {
             // the precompiled kernels then (256-thread workgroups, nothing of the tree staged)
             block = kWalkBlock;
             tree_lds = tree_verts = 0;
@@ -967,8 +988,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
                             h->jit_error.c_str());
             break;
         }
-        lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jit_const_dirichlet(nd_),
-                             jit_const_neumann(mode, nn_), gpoly, block, tree_verts);
+        lds = walk_lds_bytes(mode, nd_, nn_, (int)n_points, tree_lds, jit_const_dirichlet(O, nd_),
+                             jit_const_neumann(O, mode, nn_), gpoly, block, tree_verts) + (size_t)O.lds_pad_bytes;
         HIP_TRY(occupancy());
     }
     if (!jfn)
@@ -1009,34 +1030,30 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.tree_lds_records = tree_lds;
         a.tree_lds_verts = tree_verts;
         a.tree_depth = h->tree.depth;
-        // walk pools (wost_walk.h): near = within WOST_POOL_NEAR (default 0.1) of the Neumann
-        // polyline's largest extent from its bounding box; WOST_TREE_POOL=0 turns them off,
-        // WOST_POOL_SLOTS (default 128) walks per class and workgroup
-        const char* pe = std::getenv("WOST_TREE_POOL");
-        if (!(pe && std::atoi(pe) == 0) && h->nverts.size() >= 4) {
+        // walk pools (wost_walk.h): near = within pool_near (default 0.1) of the Neumann
+        // polyline's largest extent from its bounding box; tree_pool = 0 turns them off,
+        // pool_slots (default 128) walks per class and workgroup
+        if (O.tree_pool != 0 && h->nverts.size() >= 4) {
             float x0 = h->nverts[0], x1 = x0, y0 = h->nverts[1], y1 = y0;
             for (size_t i = 2; i + 1 < h->nverts.size(); i += 2) {
                 x0 = std::min(x0, h->nverts[i]); x1 = std::max(x1, h->nverts[i]);
                 y0 = std::min(y0, h->nverts[i + 1]); y1 = std::max(y1, h->nverts[i + 1]);
             }
-            float frac = 0.1f;
-            if (const char* e = std::getenv("WOST_POOL_NEAR")) frac = std::max(0.0f, (float)std::atof(e));
-            int slots = 128;
-            if (const char* e = std::getenv("WOST_POOL_SLOTS")) slots = std::max(1, std::min(4096, std::atoi(e)));
+            const float frac = (float)O.pool_near;
+            const int slots = O.pool_slots;
             const float m = frac * std::max(x1 - x0, y1 - y0);
-            // (study builds, WOST_TREE_ITER_STATS=1: 16 counter words after each workgroup's pools)
-            const int64_t words = (int64_t)pool_wg_words(ns, slots) + (tree_iter_stats() ? 16 : 0);
+            // (study builds, tree_iter_stats: 16 counter words after each workgroup's pools)
+            const int64_t words = (int64_t)pool_wg_words(ns, slots) + (O.tree_iter_stats ? 16 : 0);
             if ((rc = ensure_cap(h->d_pool, h->pool_cap, words * (int64_t)blocks_per_cu * h->num_cus)) != WOST_OK)
                 return rc;
             a.pool = h->d_pool;
             a.pool_slots = slots;
             a.pool_wg_words = (int32_t)words;
             a.pool_box = make_float4(x0 - m, y0 - m, x1 + m, y1 + m);
-            if (tree_iter_stats())
+            if (O.tree_iter_stats)
                 HIP_TRY(hipMemsetAsync(h->d_pool, 0, sizeof(uint32_t) * (size_t)(words * blocks_per_cu * h->num_cus),
                                        h->stream));
-            a.pool_near_waves = 2;   // WOST_POOL_NEAR_WAVES (0: by majority)
-            if (const char* e = std::getenv("WOST_POOL_NEAR_WAVES")) a.pool_near_waves = std::max(0, std::atoi(e));
+            a.pool_near_waves = O.pool_near_waves;   // (0: by majority)
         }
     }
 
@@ -1104,26 +1121,27 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         HIP_TRY(hipMemcpyAsync(h->d_begin, pin_begin, sizeof(int64_t) * (nb + 1), hipMemcpyHostToDevice, h->stream));
         // the queue head: zeroed by the previous launch's block reduce, or here after a
         // solve that stopped between a walk launch and its reduce
-        if (!h->counter_zero) HIP_TRY(hipMemsetAsync(h->d_counter, 0, sizeof(unsigned long long), h->stream));
+        if (!h->counter_zero)
+            HIP_TRY(hipMemsetAsync(h->d_counter, 0, sizeof(unsigned long long) * kCtlWords, h->stream));
         h->counter_zero = false;
 
         a.out_val = h->d_val;
         a.out_steps = h->d_steps;
         a.count = count;
-        // The launch's shape from the handle's previous solve (its mean steps per walk; 0:
-        // none). Short walks (< 32 steps; with no previous solve: no Neumann boundary) are
-        // cheap enough that the queue's shared counter and the launch's tail set the time.
-        const double prev_steps = h->last_steps_per_walk;
-        const bool short_walks = prev_steps > 0.0 ? prev_steps < 32.0 : !mode_neu(mode);
-        // Resident workgroups: after a solve of short walks, few of them per lane (C2: 640k
-        // walks, ~1.2 per lane at full occupancy) leave the launch as long as its longest
-        // walk chains, whose steps run faster with fewer waves per SIMD: ~4 walks per lane,
-        // at least 2 workgroups per CU (C2: 0.21 -> 0.18 ms per launch, profiles/r05_ab/grid_c2/)
+        // The launch's shape is a function of this call alone (never of an earlier solve:
+        // the reference calls solve() once per script, so the first call is the one that
+        // counts). Walks without a Neumann boundary (Laplace, Poisson, delta tracking on a
+        // Dirichlet-only domain) are short (13-17 steps); those with one (C3's circle, the
+        // DCR scenarios, C5) run 17-208.
+        const bool short_walks = !mode_neu(mode);
+        // Resident workgroups: few short walks per lane (C2: 640k walks, ~1.2 per lane at
+        // full occupancy) leave the launch as long as its longest walk chains, whose steps
+        // run faster with fewer waves per SIMD: ~4 walks per lane, at least 2 workgroups per
+        // CU (C2: 0.21 -> 0.18 ms per launch, profiles/r05_ab/grid_c2/)
         int64_t bpc = blocks_per_cu;
-        if (prev_steps > 0.0 && short_walks && bpc > 2)
+        if (short_walks && bpc > 2)
             bpc = std::max<int64_t>(2, std::min<int64_t>(bpc, count / ((int64_t)h->num_cus * block * 4)));
-        if (const char* e = std::getenv("WOST_GRID_BLOCKS_PER_CU"))   // A/B: fewer resident workgroups
-            bpc = std::max<int64_t>(1, std::min<int64_t>((int64_t)blocks_per_cu, std::atoi(e)));
+        if (O.grid_blocks_per_cu > 0) bpc = std::max<int64_t>(1, std::min<int64_t>(blocks_per_cu, O.grid_blocks_per_cu));
         const int64_t max_grid = bpc * h->num_cus;
         const int64_t want = (count + block - 1) / block;
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
@@ -1133,36 +1151,45 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         // counter serialises at its address (~11-16 ns): C2's 640k walks took 34k dequeues of
         // 19 walks, all waves hitting the counter at the launch's start, 0.60 ms for 47 us of
         // work (profiles/r05_ab/queue_chunk/, queue_static/).
-        // - static chunks for short walks only: long walks lose by them when launches run
-        //   concurrently (the C5 survey's handle pairs: a late-starting wave still owns its 64
-        //   walks; 1.38e10 -> 1.34e10, profiles/r05_ab/queue_c5/);
-        // - the dynamic chunk's floor: 1024 / (previous mean steps per walk) within [1, 64]
-        //   (no previous solve: 64, or 1 with a Neumann boundary, whose walks -- C4, the DCR
-        //   notebook, C5 -- run 76-208 steps): chunks below 64 walks (several dequeues per
-        //   refill) cost short walks the counter's time and balance long walks' launch ends.
-        int64_t chunk0 = short_walks ? std::min<int64_t>(64, (count + waves - 1) / waves) : 0;
-        if (const char* e = std::getenv("WOST_CHUNK0")) chunk0 = std::max(0, std::min(1024, std::atoi(e)));   // A/B
-        int64_t chunk_min = prev_steps > 0.0 ? (int64_t)std::max(1.0, std::min(64.0, 1024.0 / prev_steps))
-                                             : (mode_neu(mode) ? 1 : 64);
-        // and at most ~40M dequeues per second at the previous solve's rate: cheap short walks
-        // (Laplace, Poisson: ~2e11 walk-steps/s at ~14 steps per walk) need chunks of
-        // several hundred walks, or the counter sets the pace (64-walk chunks: 2.1e11 ->
-        // 7.0e10 walk-steps/s, profiles/r05_ab/chunk_cap/scenarios_cap64.log)
-        if (prev_steps > 0.0 && h->last_steps_per_s > 0.0)
-            chunk_min = std::max<int64_t>(chunk_min, std::min<int64_t>(1024, (int64_t)std::ceil(
-                                                         h->last_steps_per_s / (prev_steps * 4.0e7))));
-        if (const char* e = std::getenv("WOST_CHUNK_MIN")) chunk_min = std::max(1, std::min(1024, std::atoi(e)));   // A/B
+        // - static chunks except for the segment-tree kernels: their long walks lose by them
+        //   when launches run concurrently (the C5 survey's handle pairs: a late-starting
+        //   wave still owns its 64 walks; 1.38e10 -> 1.34e10, profiles/r05_ab/queue_c5/);
+        // - the dequeue's size: max(floor, min(cap, count / (waves * 4))), floor 64 for short
+        //   walks and 1 otherwise; cap 64 walks (one per lane), 16 for the segment-tree
+        //   kernels' long walks (C5: 208 steps; a wave's last chunk is work no other wave can
+        //   take: the survey 1.42e10 -> 1.46e10, profiles/r05_ab/chunk_cap/); each wave then
+        //   raises it to the floor its measured walk rate needs (WalkArgs::adaptive).
+        int64_t chunk0 = mode_tree(mode) ? 0 : std::min<int64_t>(64, (count + waves - 1) / waves);
+        if (O.chunk0 >= 0) chunk0 = O.chunk0;
+        const int64_t share = std::max<int64_t>(1, std::min<int64_t>(1 << 20, count / (waves * 4)));
+        int64_t chunk_min = short_walks ? 64 : 1;
+        if (O.chunk_min >= 1) chunk_min = O.chunk_min;
+        int64_t chunk_max = mode_tree(mode) ? 16 : 64;
+        if (O.chunk_max >= 1) chunk_max = O.chunk_max;
         a.chunk0 = (int32_t)chunk0;
         a.queue_base = waves * chunk0;
-        // the cap: a wave's last chunk is work no other wave can take when the queue runs out;
-        // 64 walks (one per lane) instead of 1,024: C4 1.26e11 -> 1.31e11, C3 4.74e10 ->
-        // 5.20e10 walk-steps/s; after walks of >= 128 steps 16 (their dequeues are rare):
-        // the C5 survey 1.42e10 -> 1.46e10 (profiles/r05_ab/chunk_cap/)
-        int64_t chunk_max = prev_steps >= 128.0 ? 16 : 64;
-        if (const char* e = std::getenv("WOST_CHUNK_MAX")) chunk_max = std::max(1, std::min(1 << 20, std::atoi(e)));   // A/B
-        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(chunk_max, count / (waves * 4)));
+        a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(chunk_max, share));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
         // on C4 and 10-14% slower on the short-walk scenarios: profiles/r02_ab/guided_queue.log)
+        // (the waves' rate floor assumes the 100 MHz wall clock of gfx950)
+        const bool adaptive = O.adaptive_chunk != 0 && O.chunk_min < 1 && O.chunk_max < 1 && h->tick_khz == 100000.0;
+        a.chunk_share = adaptive ? (uint32_t)std::max<int64_t>(share, a.chunk) : 0u;
+        a.waves = (uint32_t)std::min<int64_t>(waves, INT32_MAX);
+        if ((int64_t)ctl_words(waves) > h->ctl_cap) {   // more waves than the control block holds
+            HIP_TRY(hipStreamSynchronize(h->stream));
+            (void)hipFree(h->d_counter);
+            h->d_counter = nullptr;
+            h->ctl_cap = 0;
+            HIP_TRY(hipMalloc(&h->d_counter, sizeof(unsigned long long) * ctl_words(waves)));
+            HIP_TRY(hipMemset(h->d_counter, 0, sizeof(unsigned long long) * ctl_words(waves)));
+            h->ctl_cap = (int64_t)ctl_words(waves);
+            a.counter = h->d_counter;
+        }
+        h->timing.blocks_per_cu = (int32_t)bpc;
+        h->timing.block_threads = block;
+        h->timing.chunk0 = (int32_t)chunk0;
+        h->timing.chunk = a.chunk;
+        h->timing.adaptive = adaptive ? 1 : 0;
         h->timing.grid_blocks = grid;
 
         HIP_TRY(hipEventRecord(h->ev[0], h->stream));
@@ -1173,8 +1200,9 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
             HIP_TRY(launch_walk(mode, a, grid, h->stream));
         }
         HIP_TRY(hipEventRecord(h->ev[1], h->stream));
-        HIP_TRY(launch_block_reduce(h->d_val, h->d_steps, h->d_begin, nb, ns, h->d_bstats + row * (j - block_begin),
-                                    h->d_counter, h->stream));
+        HIP_TRY(launch_block_reduce(h->d_val, h->d_steps, h->d_begin, nb, ns, d_rows + row * (j - block_begin),
+                                    h->d_counter, h->stream, mode_tree(mode) ? 0 : waves, d_lstats,
+                                    launches == 0 ? 1 : 0));   // (the tree kernels keep no wave records)
         h->counter_zero = true;
         HIP_TRY(hipEventRecord(h->ev[2], h->stream));
         if (walk_values)
@@ -1187,7 +1215,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
                                    hipMemcpyDeviceToHost, h->stream));
         const bool last = j2 >= block_end;
         if (last) {   // the block sums ride the same wait
-            HIP_TRY(hipMemcpyAsync(pin_bstats, h->d_bstats, sizeof(double) * row * nblk, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipMemcpyAsync(pin_bstats, h->d_bstats, sizeof(double) * (kLstatsWords + row * nblk),
+                                   hipMemcpyDeviceToHost, h->stream));
             HIP_TRY(hipEventRecord(h->ev[5], h->stream));
             HIP_TRY(hipEventSynchronize(h->ev[5]));
         } else {
@@ -1202,7 +1231,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         walks_done += count;
         j = j2;
     }
-    if (tree_iter_stats() && a.pool != nullptr) {   // study builds: the tree queries' loop counters
+    if (O.tree_iter_stats && a.pool != nullptr) {   // study builds: the tree queries' loop counters
         const int64_t nwg = (int64_t)blocks_per_cu * h->num_cus;
         std::vector<uint32_t> pw((size_t)(a.pool_wg_words * nwg));
         HIP_TRY(hipMemcpy(pw.data(), a.pool, sizeof(uint32_t) * pw.size(), hipMemcpyDeviceToHost));
@@ -1214,7 +1243,18 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %.0f", c[i]);
         std::fprintf(stderr, "\n");
     }
-    const double* bs = pin_bstats;   // (copied and waited for with the last batch)
+    const double* bs = pin_bstats + kLstatsWords;   // (copied and waited for with the last batch)
+    {   // the launch statistics (wost_kernels.hip reduce_wave_stats), wall-clock ticks
+        unsigned long long ls[kLstatsWords];
+        std::memcpy(ls, pin_bstats, sizeof(ls));
+        const double ms_per_tick = 1.0 / h->tick_khz;
+        h->timing.max_walk_steps = (uint32_t)std::min<unsigned long long>(ls[3], 0xFFFFFFFFull);
+        h->timing.span_ms = ls[2] > ls[0] ? (double)(ls[2] - ls[0]) * ms_per_tick : 0.0;
+        h->timing.tail_ms = ls[2] > ls[1] ? (double)(ls[2] - ls[1]) * ms_per_tick : 0.0;
+        h->timing.last_wave_ms = (double)ls[5] * ms_per_tick;
+        h->timing.last_wave_iters = (uint32_t)ls[4];
+        h->timing.max_wave_iters = (uint32_t)ls[6];
+    }
     float tt = 0.f;
     HIP_TRY(hipEventElapsedTime(&tt, h->ev[4], h->ev[5]));
 
@@ -1233,8 +1273,7 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     h->timing.n_launches = launches;
     h->timing.total_steps = steps_sum;
     h->timing.total_walks = (uint64_t)walks_total;
-    if (walks_total > 0) h->last_steps_per_walk = (double)steps_sum / (double)walks_total;
-    h->last_steps_per_s = walk_ms > 0.0 ? (double)steps_sum / (walk_ms * 1e-3) : 0.0;
+    h->timing.jit_ms = jit_ms;
     h->timing.jit = jfn ? 1 : 0;
     h->timing.tree = mode_tree(mode) ? 1 : 0;
     return WOST_OK;
@@ -1300,6 +1339,18 @@ int wost_solve_range(wost_handle* h, const float* points, int64_t n_points, int6
         acc.grid_blocks = h->timing.grid_blocks;
         acc.jit = h->timing.jit;
         acc.tree = h->timing.tree;
+        acc.blocks_per_cu = h->timing.blocks_per_cu;
+        acc.block_threads = h->timing.block_threads;
+        acc.chunk0 = h->timing.chunk0;
+        acc.chunk = h->timing.chunk;
+        acc.adaptive = h->timing.adaptive;
+        acc.max_walk_steps = std::max(acc.max_walk_steps, h->timing.max_walk_steps);
+        acc.jit_ms += h->timing.jit_ms;
+        acc.span_ms += h->timing.span_ms;
+        acc.tail_ms = h->timing.tail_ms;
+        acc.last_wave_ms = h->timing.last_wave_ms;
+        acc.last_wave_iters = h->timing.last_wave_iters;
+        acc.max_wave_iters = std::max(acc.max_wave_iters, h->timing.max_wave_iters);
     }
     if (block_stats) std::memcpy(block_stats, all.data(), sizeof(double) * all.size());
     if (point_stats) {
@@ -1371,17 +1422,17 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
         const float2 n = segment_left_normal(a, b);
         phi[i] = std::atan2(n.y, n.x);
     }
-    // offline study of the tree kernels' LDS staging (tools/jit_isa.py --stage): the source
-    // of staging level WOST_KERNEL_SOURCE_STAGE (2: records and vertices, 1: records, with
-    // WOST_TREE_LDS_BLOCK's workgroup) instead of the 256-thread unstaged kernel
+    // study builds: offline study of the tree kernels' LDS staging (tools/jit_isa.py --stage):
+    // the source of staging level WOST_KERNEL_SOURCE_STAGE (2: records and vertices, 1:
+    // records, with the tree_lds_block workgroup) instead of the 256-thread unstaged kernel
     int stage = 0, block = kWalkBlock;
+#if defined(WOST_STUDY)
     if (const char* e = std::getenv("WOST_KERNEL_SOURCE_STAGE"); e && mode_tree(mode)) {
         stage = std::max(0, std::min(2, std::atoi(e)));
-        block = stage == 2 ? kTreeStageVertsBlock : stage == 1 ? kTreeStageBlock : kWalkBlock;
-        if (const char* b = std::getenv("WOST_TREE_LDS_BLOCK"); b && stage == 1)
-            block = std::max(64, std::min(1024, std::atoi(b) / 64 * 64));
+        block = stage == 2 ? kTreeStageVertsBlock : stage == 1 ? h->opt.tree_lds_block : kWalkBlock;
     }
-    const std::string src = jit_generate(mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
+#endif
+    const std::string src = jit_generate(h->opt, mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
                                          (int)(h->dverts.size() / 2), h->nverts.data(), nn, false, 1, block,
                                          phi.empty() ? nullptr : phi.data(), false, stage, exact_trig_of(h));
     delete h;
@@ -1426,6 +1477,41 @@ int wost_set_jit(wost_handle* h, int32_t enable) {
     h->jit_enabled = enable != 0;
     h->jit_fn = nullptr;
     h->jit_mode = -1;
+    return WOST_OK;
+}
+
+int wost_set_option(wost_handle* h, const char* name, double value) {
+    if (!h || !name) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    bool kernel = false;
+    const int rc = options_set(h->opt, name, value, &kernel);
+    if (rc == -1) return fail(WOST_ERR_INVALID_ARG, "unknown option \"%s\" (wost_options.h)", name);
+    if (rc == -2) return fail(WOST_ERR_INVALID_ARG, "option \"%s\": value %g out of range", name, value);
+    if (rc == -3)
+        return fail(WOST_ERR_UNSUPPORTED, "option \"%s\" exists in study builds only (make study)", name);
+    if (kernel) {   // the generated source changes: rebuild the handle's kernel
+        h->jit_fn = nullptr;
+        h->jit_mode = -1;
+    }
+    return WOST_OK;
+}
+
+int wost_get_option(const wost_handle* h, const char* name, double* value) {
+    if (!h || !name || !value) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    if (options_get(h->opt, name, value) != 0) return fail(WOST_ERR_INVALID_ARG, "unknown option \"%s\"", name);
+    return WOST_OK;
+}
+
+int wost_options_report(const wost_handle* h, char* out, int64_t capacity, int64_t* length) {
+    if (!length) return fail(WOST_ERR_INVALID_ARG, "NULL length");
+    Options fresh;   // without a handle: what a new handle gets (study builds: from the environment)
+    options_from_study_env(fresh);
+    const std::string r = options_report(h ? h->opt : fresh);
+    *length = (int64_t)r.size();
+    if (out && capacity > 0) {
+        const size_t n = std::min<size_t>(r.size(), (size_t)capacity - 1);
+        std::memcpy(out, r.data(), n);
+        out[n] = '\0';
+    }
     return WOST_OK;
 }
 

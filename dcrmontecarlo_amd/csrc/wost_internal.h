@@ -84,10 +84,14 @@ hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s);
 // Per-block reduction: block b covers local walks [begin[b], begin[b+1]).
 // ns values per walk (multi-source: val[walk * ns + k]); rows of 2*ns+1 doubles
 // (sum_k, sumsq_k for each k, then steps).
-// counter_reset (may be null): the walk queue's head, set to 0 for the next walk launch
+// ctl (may be null): the walk launch's control words (wost_walk.h kCtlWords), the queue
+// head reset for the next walk launch. lstats (may be null): the solve's launch statistics
+// [8] (wost_kernels.hip reduce_wave_stats) from the walk launch's n_waves per-wave records
+// and its walks' step counts; first_batch: the solve's first launch.
 hipError_t launch_block_reduce(const float* val, const uint32_t* steps, const int64_t* begin,
-                               int64_t nblocks, int ns, double* out, unsigned long long* counter_reset,
-                               hipStream_t s);
+                               int64_t nblocks, int ns, double* out, unsigned long long* ctl,
+                               hipStream_t s, int64_t n_waves = 0, unsigned long long* lstats = nullptr,
+                               int first_batch = 1);
 
 hipError_t launch_geometry_query(int op, const float2* verts, int nv, const float2* pts,
                                  const float2* dirs, const float* radii, int64_t n,

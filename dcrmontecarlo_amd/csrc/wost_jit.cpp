@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -30,8 +31,8 @@ namespace {
 // (q = RN(duv y)) equals RN(duv / duu) for every duv mantissa (checked
 // exhaustively, once per mantissa of duu, cached), else 0 (wost_device.h
 // poly_distance_rcp). duu is formed exactly like the kernel forms it.
-// A/B switches for tools/ab_bench.sh (WOST_EXP_FLAGS, a bit mask; 0 in
-// production): 1 generic poly_distance for compiled-in polylines, 2 IEEE
+// A/B switches for tools/ab_bench.sh (Options::exp_flags, a bit mask: study builds
+// only, from WOST_EXP_FLAGS; always 0 in the product library): 1 generic poly_distance for compiled-in polylines, 2 IEEE
 // unit_direction. Ablations (timing studies only: the results are WRONG, the
 // walks merely stay statistically alike): 4 a cheap hash instead of Philox, 8 no
 // alpha(z) evaluation, 16 no sigma' at collisions, 32 no Neumann ray query;
@@ -48,10 +49,6 @@ namespace {
 // silhouette scan instead of silhouette_distance_compact; ablation 65536 no
 // silhouette query (dn = +inf).
 // Each bit only selects one fixed code path.
-int exp_flags() {
-    const char* e = std::getenv("WOST_EXP_FLAGS");
-    return e ? (int)std::strtol(e, nullptr, 10) & 0x3FFFFFFF : 0;
-}
 
 // the squared segment length exactly as the kernel forms it
 float segment_duu(float ax, float ay, float bx, float by) {
@@ -203,9 +200,9 @@ std::string sat_call(const DFactor& f) {
 // predicate and the coefficients are finite, a wave whose lanes are all saturated
 // returns {value, z, z, z} (wost_device.h, whole-field saturation): the value from
 // `value_fn` (the field's value body, the same bits as the jet's value there).
-std::string jet_body(const DField& fd, const DTerm* terms, const DFactor* factors, const char* value_fn = nullptr) {
+std::string jet_body(const DField& fd, const DTerm* terms, const DFactor* factors, const char* value_fn, int xflags) {
     std::ostringstream o;
-    if (value_fn != nullptr && !(exp_flags() & 512)) {
+    if (value_fn != nullptr && !(xflags & 512)) {
         std::ostringstream s;
         bool ok = fd.n_terms > 0, radial = false;
         for (int t = 0; t < fd.n_terms && ok; ++t) {
@@ -304,35 +301,32 @@ const char* const kCompileOptions[] = {"-O3", "-std=c++17", "-fhip-fp32-correctl
                                        "-ffp-contract=fast-honor-pragmas"};
 constexpr int kCacheFormat = 2;   // bump when the generator or the cached file layout changes
 
-// A/B only: WOST_JIT_SCHED=<strategy> adds -mllvm -amdgpu-sched-strategy=<strategy>
-// (max-ilp, max-memory-clause, iterative-ilp, ...) to the hiprtc options.
-std::string sched_option() {
-    const char* e = std::getenv("WOST_JIT_SCHED");
-    return e && *e ? std::string("-amdgpu-sched-strategy=") + e : std::string();
+// Study builds only: Options::jit_sched (WOST_JIT_SCHED=<strategy>) adds -mllvm
+// -amdgpu-sched-strategy=<strategy> (max-ilp, max-memory-clause, iterative-ilp, ...).
+std::string sched_option(const Options& opt) {
+    return !opt.jit_sched.empty() ? std::string("-amdgpu-sched-strategy=") + opt.jit_sched : std::string();
 }
 
 // -fno-slp-vectorize: no packed FP32 (v_pk_*) from the SLP vectoriser. On gfx950 a
 // v_pk_{add,mul,fma}_f32 issues in the time of two scalar ones, and the pairs of
 // constants it wants in SGPRs pushed the long unrolled scans (C3's 32-segment ray
 // query, the tree traversal) past the SGPR budget into v_writelane/v_readlane
-// spills. A/B only: WOST_JIT_SLP=1 keeps the vectoriser.
-bool slp_off() {
-    const char* e = std::getenv("WOST_JIT_SLP");
-    return !(e && *e == '1');
-}
+// spills. Options::jit_slp = 1 keeps the vectoriser (A/B).
+bool slp_off(const Options& opt) { return opt.jit_slp == 0; }
 
-std::string cache_identity() {
+std::string cache_identity(const Options& opt) {
     std::string id = "fmt" + std::to_string(kCacheFormat);
     for (const char* o : kCompileOptions) id += std::string("|") + o;
-    if (!sched_option().empty()) id += "|-mllvm " + sched_option();
-    if (slp_off()) id += "|-fno-slp-vectorize";
+    if (!sched_option(opt).empty()) id += "|-mllvm " + sched_option(opt);
+    if (slp_off(opt)) id += "|-fno-slp-vectorize";
     int maj = 0, min = 0, rt = 0;
     if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) id += "|hiprtc" + std::to_string(maj) + "." + std::to_string(min);
     if (hipRuntimeGetVersion(&rt) == hipSuccess) id += "|hip" + std::to_string(rt);
     return id;
 }
 
-bool compile(const std::string& src, const std::string& arch, std::vector<char>& code, std::string* err) {
+bool compile(const Options& opt, const std::string& src, const std::string& arch, std::vector<char>& code,
+             std::string* err) {
     const char* hdrs[] = {wost_embedded_wost_h, wost_embedded_wost_device_h, wost_embedded_wost_walk_h};
     const char* names[] = {"wost.h", "wost_device.h", "wost_walk.h"};
     hiprtcProgram prog;
@@ -343,8 +337,8 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
     std::string arch_opt = "--offload-arch=" + arch;
     std::vector<const char*> opts = {arch_opt.c_str()};
     for (const char* o : kCompileOptions) opts.push_back(o);
-    if (slp_off()) opts.push_back("-fno-slp-vectorize");
-    const std::string sched = sched_option();
+    if (slp_off(opt)) opts.push_back("-fno-slp-vectorize");
+    const std::string sched = sched_option(opt);
     if (!sched.empty()) {
         opts.push_back("-mllvm");
         opts.push_back(sched.c_str());
@@ -369,25 +363,19 @@ bool compile(const std::string& src, const std::string& arch, std::vector<char>&
 
 }  // namespace
 
-int jit_const_vertices() {
-    int max_const = kJitMaxConstVertices;   // A/B knob: WOST_JIT_CONST_VERTICES (an integer)
-    if (const char* e = std::getenv("WOST_JIT_CONST_VERTICES")) max_const = std::max(0, std::min(256, std::atoi(e)));
-    return max_const;
+bool jit_const_dirichlet(const Options& o, int nd) { return nd <= o.const_vertices; }
+
+bool jit_const_neumann(const Options& o, int mode, int nn) {
+    return mode_neu(mode) && !mode_tree(mode) && nn >= 1 && nn <= o.const_vertices;
 }
 
-bool jit_const_dirichlet(int nd) { return nd <= jit_const_vertices(); }
-
-bool jit_const_neumann(int mode, int nn) {
-    return mode_neu(mode) && !mode_tree(mode) && nn >= 1 && nn <= jit_const_vertices();
+bool jit_fused_neumann_scan(const Options& o, int mode, int nn) {
+    // (Options::fused_scan = 0: the two separate scans, the round-4 kernel; same bits)
+    return mode_neu(mode) && !mode_tree(mode) && !mode_fix(mode) && !jit_const_neumann(o, mode, nn) && nn >= 66 &&
+           o.fused_scan != 0;
 }
 
-bool jit_fused_neumann_scan(int mode, int nn) {
-    // (WOST_EXP_FLAGS 2^28: the two separate scans, A/B)
-    return mode_neu(mode) && !mode_tree(mode) && !mode_fix(mode) && !jit_const_neumann(mode, nn) && nn >= 66 &&
-           !(exp_flags() & (1 << 28));
-}
-
-std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
+std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record, int n_sources,
                          int block, const float* seg_phi, bool global_polylines, int tree_stage,
                          bool exact_trig) {
@@ -400,40 +388,33 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     const DField& fS = hdr.field[SLOT_SIGMA];
     const DField& fA = hdr.field[SLOT_ALPHA];
     std::ostringstream o;
-    if (exp_flags() & 2) o << "#define WOST_EXP_IEEE_DIRECTION 1\n";
-    if (exp_flags() & 4096) o << "#define WOST_NO_TREE_BEHIND 1\n";   // A/B: line pruning only
-    if (exp_flags() & 4) o << "#define WOST_ABL_NO_PHILOX 1\n";
-    if (exp_flags() & 8) o << "#define WOST_ABL_NO_ALPHA_Z 1\n";
-    if (exp_flags() & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
-    if (exp_flags() & 32) o << "#define WOST_ABL_NO_RAY 1\n";
-    if (exp_flags() & 65536) o << "#define WOST_ABL_NO_SILHOUETTE 1\n";
-    if (exp_flags() & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
-    if (exp_flags() & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
-    if (exp_flags() & (1 << 29)) o << "#define WOST_EXP_UNIT_TAB 1\n";   // A/B: unit_direction's (n, y) table
-    if (exp_flags() & 131072) o << "#define WOST_EXP_SCAN_BITS 1\n";   // A/B: neumann_scan_both's per-vertex bits
-    if ((exp_flags() >> 18) & 1023) o << "#define WOST_ABL_DUP " << ((exp_flags() >> 18) & 1023) << "\n";   // phase_dup.sh
+    const int xf = opt.exp_flags;   // study builds only (0 in the product library)
+    if (xf & 2) o << "#define WOST_EXP_IEEE_DIRECTION 1\n";
+    if (xf & 4096) o << "#define WOST_NO_TREE_BEHIND 1\n";   // A/B: line pruning only
+    if (xf & 4) o << "#define WOST_ABL_NO_PHILOX 1\n";
+    if (xf & 8) o << "#define WOST_ABL_NO_ALPHA_Z 1\n";
+    if (xf & 16) o << "#define WOST_ABL_NO_SIGMA_PRIME 1\n";
+    if (xf & 32) o << "#define WOST_ABL_NO_RAY 1\n";
+    if (xf & 65536) o << "#define WOST_ABL_NO_SILHOUETTE 1\n";
+    if (xf & 64) o << "#define WOST_EXP_PARTIAL_UNROLL 1\n";
+    if (xf & 128) o << "#define WOST_EXP_LIBM_SINCOS 1\n";
+    if (xf & (1 << 29)) o << "#define WOST_EXP_UNIT_TAB 1\n";   // A/B: unit_direction's (n, y) table
+    if (xf & 131072) o << "#define WOST_EXP_SCAN_BITS 1\n";   // A/B: neumann_scan_both's per-vertex bits
+    if ((xf >> 18) & 1023) o << "#define WOST_ABL_DUP " << ((xf >> 18) & 1023) << "\n";   // phase_dup.sh
     o << "#define WOST_JIT_TRIG_EXACT " << (exact_trig ? 1 : 0) << "\n";   // wost_set_trig
-    if (exp_flags() & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
-    if (const char* e = std::getenv("WOST_JIT_PHILOX_AHEAD"))   // A/B: Philox one step ahead
-        o << "#define WOST_PHILOX_AHEAD " << std::max(0, std::min(3, std::atoi(e))) << "\n";
-    if (const char* e = std::getenv("WOST_JIT_REFILL_MIN"))   // A/B: refill batch size
-        o << "#define WOST_REFILL_MIN " << std::max(1, std::min(64, std::atoi(e))) << "\n";
-    if (const char* e = std::getenv("WOST_JIT_TREE_SHARE"))   // A/B: tree hand-out threshold (0: none)
-        o << "#define WOST_TREE_SHARE " << std::max(0, std::min(64, std::atoi(e))) << "\n";
-    if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_DESCENT"))   // A/B: hand-outs during the descent
-        o << "#define WOST_TREE_SHARE_DESCENT " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
-    if (const char* e = std::getenv("WOST_JIT_POOL_MIN_PUSH"))   // A/B: fewest walks a wave parks
-        o << "#define WOST_POOL_MIN_PUSH " << std::max(1, std::min(64, std::atoi(e))) << "\n";
-    if (const char* e = std::getenv("WOST_TREE_ITER_STATS"))   // study build: loop counters
-        if (std::atoi(e) == 1 && tree) o << "#define WOST_TREE_ITER_STATS 1\n";
+    if (xf & 2048) o << "#define WOST_EXP_IEEE_SQRT 1\n";
+    // the handle's bit-preserving kernel options (wost_set_option; -1: the kernel's default)
+    if (opt.philox_ahead >= 0) o << "#define WOST_PHILOX_AHEAD " << opt.philox_ahead << "\n";
+    if (opt.refill_min >= 1) o << "#define WOST_REFILL_MIN " << opt.refill_min << "\n";
+    if (opt.tree_share >= 0) o << "#define WOST_TREE_SHARE " << opt.tree_share << "\n";
+    if (opt.tree_share_descent >= 0) o << "#define WOST_TREE_SHARE_DESCENT " << opt.tree_share_descent << "\n";
+    if (opt.pool_min_push != 1) o << "#define WOST_POOL_MIN_PUSH " << opt.pool_min_push << "\n";
+    if (opt.tree_iter_stats && tree) o << "#define WOST_TREE_ITER_STATS 1\n";   // study builds: loop counters
     if (tree && tree_stage >= 1) o << "#define WOST_TREE_STAGED 1\n";    // every record in LDS
     if (tree && tree_stage >= 2) o << "#define WOST_TREE_VSTAGED 1\n";   // and the Neumann vertices
-    if (const char* e = std::getenv("WOST_JIT_TREE_QMARGIN"))   // A/B: per-query rounding scales
-        o << "#define WOST_TREE_QMARGIN " << (std::atoi(e) != 0 ? 1 : 0) << "\n";
-    if (const char* e = std::getenv("WOST_JIT_TREE_SHARE_MIN"))   // A/B: fewest subtrees worth a hand-out
-        o << "#define WOST_TREE_SHARE_MIN " << std::max(1, std::min(64, std::atoi(e))) << "\n";
-    if (const char* e = std::getenv("WOST_JIT_TREE_BATCH"))   // A/B: children loaded per batch
-        o << "#define WOST_TREE_BATCH " << (std::atoi(e) >= 4 ? 4 : std::atoi(e) >= 2 ? 2 : 1) << "\n";
+    if (opt.tree_qmargin >= 0) o << "#define WOST_TREE_QMARGIN " << opt.tree_qmargin << "\n";
+    if (opt.tree_share_min >= 1) o << "#define WOST_TREE_SHARE_MIN " << opt.tree_share_min << "\n";
+    if (opt.tree_batch >= 1) o << "#define WOST_TREE_BATCH " << (opt.tree_batch >= 4 ? 4 : opt.tree_batch >= 2 ? 2 : 1) << "\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
       << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
@@ -456,7 +437,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    __device__ __forceinline__ float alpha(float x, float y) const {\n"
       << (fA.present ? value_body(fA, terms, factors) : "        return 1.0f;\n") << "    }\n";
     o << "    __device__ __forceinline__ wost::Jet alpha_jet(float x, float y) const {\n"
-      << (fA.present ? jet_body(fA, terms, factors, (fA.flags & WOST_FIELD_DETACHED) ? nullptr : "alpha") : "        return wost::jet_const(1.0f);\n") << "    }\n";
+      << (fA.present ? jet_body(fA, terms, factors, (fA.flags & WOST_FIELD_DETACHED) ? nullptr : "alpha", xf) : "        return wost::jet_const(1.0f);\n") << "    }\n";
     o << "    __device__ __forceinline__ bool detached() const { return "
       << ((fA.flags & WOST_FIELD_DETACHED) ? "true" : "false") << "; }\n";
     o << "    __device__ __forceinline__ float sigma_bar() const { return " << lit(hdr.sigma_bar) << "; }\n";
@@ -464,15 +445,15 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    __device__ __forceinline__ float inv_sigma_bar() const { return " << lit(hdr.inv_sigma_bar) << "; }\n";
     // a short Dirichlet polyline is compiled in: the scan unrolls, the segment
     // vectors and squared lengths fold to constants (the same IEEE operations)
-    const bool dconst = jit_const_dirichlet(nd);
+    const bool dconst = jit_const_dirichlet(opt, nd);
     // a compiled-in Neumann polyline also needs its segment angles as constants
-    const bool nconst = jit_const_neumann(mode, nn) && (seg_phi != nullptr || nn < 2);
+    const bool nconst = jit_const_neumann(opt, mode, nn) && (seg_phi != nullptr || nn < 2);
     o << "    static constexpr bool kConstDirichlet = " << (dconst ? "true" : "false") << ";\n";
     o << "    static constexpr bool kConstNeumann = " << (nconst ? "true" : "false") << ";\n";
     // a long Neumann polyline scanned (no segment tree: the brute-force kernel): both
     // queries in one pass with the per-vertex line filter (neumann_scan_both);
-    // WOST_EXP_FLAGS 2^28: the two separate scans instead (A/B)
-    const bool fused = !nconst && jit_fused_neumann_scan(mode, nn);
+    // Options::fused_scan = 0: the two separate scans instead (A/B)
+    const bool fused = !nconst && jit_fused_neumann_scan(opt, mode, nn);
     o << "    static constexpr bool kFusedNeumann = " << (fused ? "true" : "false") << ";\n";
     if (fused) {
         float c1 = 0.0f;
@@ -492,7 +473,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
         o << "};\n";
         // poly_distance_const when every segment has 0 < duu and the coordinates are
         // below 2^60, with the reciprocal squared lengths for the Markstein division
-        bool ok = nd >= 2 && !(exp_flags() & 1);
+        bool ok = nd >= 2 && !(xf & 1);
         std::ostringstream r;
         for (int i = 0; i < nd && ok; ++i) ok = std::fabs(dverts[2 * i]) <= 0x1p60f && std::fabs(dverts[2 * i + 1]) <= 0x1p60f;
         for (int i = 0; ok && i + 1 < nd; ++i) {
@@ -519,7 +500,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     o << "    __device__ __forceinline__ float neumann_silhouette_distance(const float2* sN, int nn, float x, float y) const {\n";
     // 9+ compiled-in vertices: the two-pass scan (squared distances only for each
     // lane's own silhouette vertices, from the staged copy)
-    if (nconst && nn >= 9 && nn <= 66 && !(exp_flags() & 32768))
+    if (nconst && nn >= 9 && nn <= 66 && !(xf & 32768))
         o << nverts_decl() << "        return wost::silhouette_distance_compact<" << nn << ">(v, sN, x, y);\n";
     else if (nconst) o << nverts_decl() << "        return wost::silhouette_distance<" << nn << ">(v, " << nn << ", x, y);\n";
     else o << "        return wost::silhouette_distance(sN, nn, x, y);\n";
@@ -530,14 +511,14 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     // measured slower on C3's 32-segment circle: 1.24e10 vs 1.94e10 walk-steps/s)
     // 8+ compiled-in segments: the two-pass scan (C3's 32-segment circle +11%; with one or
     // two segments its loop costs more than it saves: C4 -9%, profiles/r02_ab/ray_scan_two_pass.log)
-    if (nconst && nn >= 9 && nn <= 65 && !(exp_flags() & (16384 | 8192))) {   // the per-vertex line filter
+    if (nconst && nn >= 9 && nn <= 65 && !(xf & (16384 | 8192))) {   // the per-vertex line filter
         float c1 = 0.0f;
         for (int i = 0; i < nn; ++i) c1 = std::max(c1, std::fabs(nverts[2 * i]) + std::fabs(nverts[2 * i + 1]));
         o << nverts_decl() << "        return wost::intersect_polylines_lines<" << nn << ">(v, sN, x, y, dx, dy, r, "
           << lit(c1 * 1.0001f) << ");\n";
-    } else if (nconst && nn >= 9 && nn <= 65 && !(exp_flags() & 16384))   // (16384: per-segment exact tests, A/B)
+    } else if (nconst && nn >= 9 && nn <= 65 && !(xf & 16384))   // (16384: per-segment exact tests, A/B)
         o << nverts_decl() << "        return wost::intersect_polylines_compact<" << nn << ">(v, sN, x, y, dx, dy, r);\n";
-    else if (nconst && !(exp_flags() & 1024))   // (1024: the generic unroll-by-2 scan, A/B)
+    else if (nconst && !(xf & 1024))   // (1024: the generic unroll-by-2 scan, A/B)
         o << nverts_decl() << "        return wost::intersect_polylines<false, " << nn << ">(v, " << nn
           << ", x, y, dx, dy, r);\n";
     else if (nconst) o << nverts_decl() << "        return wost::intersect_polylines<false>(v, " << nn << ", x, y, dx, dy, r);\n";
@@ -565,7 +546,7 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     // once (profiles/r03_tree/tree_batch_waves_ab.log), 4 when the tree's records are
     // staged (one 16-wave or two 8-wave workgroups per CU)
     int waves = tree ? (block != kWalkBlock ? 4 : 5) : 7;
-    if (const char* e = std::getenv("WOST_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
+    if (opt.jit_waves > 0) waves = opt.jit_waves;
     o << "extern \"C\" __global__ void __launch_bounds__(" << block << ", " << waves << ")\n"
       << "wost_walk_jit(const wost::WalkArgs A) {\n"
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
@@ -584,8 +565,9 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
     return o.str();
 }
 
-bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err,
-                    hipFunction_t* alpha_fn) {
+bool jit_get_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn, std::string* err,
+                    hipFunction_t* alpha_fn, double* compile_ms) {
+    if (compile_ms) *compile_ms = 0.0;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
         *err = "hipGetDeviceProperties failed";
@@ -595,7 +577,7 @@ bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, st
     arch = arch.substr(0, arch.find(':'));
     // the embedded headers, compile options and compiler/runtime versions are part of the
     // key: a rebuilt library, other options or a ROCm upgrade never reuse stale code
-    static const std::string ident = cache_identity();
+    const std::string ident = cache_identity(opt);
     const uint64_t h = fnv1a(source + "|" + arch + "|" + ident + "|" + wost_embedded_wost_h +
                              wost_embedded_wost_device_h + wost_embedded_wost_walk_h);
     char hex[32];
@@ -612,12 +594,17 @@ bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, st
     std::vector<char> code;
     const std::string dir = cache_dir();
     const std::string name = std::string("walk_") + arch + "_" + hex + ".hsaco";
+#if defined(WOST_STUDY)
     if (const char* dump = std::getenv("WOST_JIT_DUMP")) {   // generated source, for offline ISA study
         const std::string s(source);
         write_file_atomic(dump, std::string("walk_") + hex + ".hip", std::vector<char>(s.begin(), s.end()));
     }
+#endif
     if (dir.empty() || !read_file(dir + "/" + name, code)) {
-        if (!compile(source, arch, code, err)) return false;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (!compile(opt, source, arch, code, err)) return false;
+        if (compile_ms)
+            *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         write_file_atomic(dir, name, code);
     }
     Entry e;

@@ -15,20 +15,18 @@
 #include <string>
 
 #include "wost_device.h"
+#include "wost_options.h"
 
 namespace wost {
 
-// Polylines of at most this many vertices are compiled into the specialised
-// kernel as constants (and then not staged in LDS).
-constexpr int kJitMaxConstVertices = 40;
-// The threshold in force: kJitMaxConstVertices, or WOST_JIT_CONST_VERTICES (A/B knob).
-int jit_const_vertices();
-// Which polylines a specialised kernel of `mode` compiles in.
-bool jit_const_dirichlet(int nd);
-bool jit_const_neumann(int mode, int nn);
+// Which polylines a specialised kernel of `mode` compiles in (at most
+// Options::const_vertices vertices, default kJitMaxConstVertices; they are then not
+// staged in LDS).
+bool jit_const_dirichlet(const Options& o, int nd);
+bool jit_const_neumann(const Options& o, int mode, int nn);
 // a long Neumann polyline scanned without the segment tree (the brute-force kernel, reference
 // mode): both queries of a step in one pass (wost_device.h neumann_scan_both)
-bool jit_fused_neumann_scan(int mode, int nn);
+bool jit_fused_neumann_scan(const Options& o, int mode, int nn);
 
 // HIP source of a walk kernel named "wost_walk_jit" for walk mode `mode`
 // (wost_internal.h WalkMode) with the fields of `prog` and short polylines
@@ -43,7 +41,8 @@ bool jit_fused_neumann_scan(int mode, int nn);
 // modes): 0 = the segment tree through L1/L2, 1 = its records staged in LDS
 // (WOST_TREE_STAGED), 2 = its records and the Neumann vertices (WOST_TREE_VSTAGED) --
 // the caller's staging decision, independent of the workgroup size.
-std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
+// `opt`: the handle's kernel options (wost_options.h).
+std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, const DTerm* terms, const DFactor* factors,
                          const float* dverts, int nd, const float* nverts, int nn, bool record,
                          int n_sources = 1, int block = 256, const float* seg_phi = nullptr,
                          bool global_polylines = false, int tree_stage = 0, bool exact_trig = true);
@@ -51,7 +50,9 @@ std::string jit_generate(int mode, const DProgram& hdr, const DTerm* terms, cons
 // Compiles (or fetches from the caches) the source for `device` and returns
 // the kernel. On failure returns false and a message in *err.
 // alpha_fn (optional): the source's wost_point_alpha_jit kernel (delta tracking), or null.
-bool jit_get_kernel(int device, const std::string& source, hipFunction_t* fn, std::string* err,
-                    hipFunction_t* alpha_fn = nullptr);
+// opt: the compile options it selects (the SLP vectoriser; study builds: the scheduler).
+// *compile_ms: host time of the hiprtc compile (0 when a cache had the code).
+bool jit_get_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn, std::string* err,
+                    hipFunction_t* alpha_fn = nullptr, double* compile_ms = nullptr);
 
 }  // namespace wost

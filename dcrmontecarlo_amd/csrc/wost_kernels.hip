@@ -201,16 +201,83 @@ hipError_t launch_walk(int mode, const WalkArgs& a, int grid, hipStream_t s) {
 // ---------------------------------------------------------------------------
 constexpr int kReduceBlock = 256;
 
+// The walk launch's statistics (the per-wave records after the control words, wost_walk.h
+// kCtlWords) summed up by one workgroup: lstats[0] earliest wave start, [1] latest dequeue,
+// [2] latest wave end (wall-clock ticks), [4] loop iterations of the wave that ended last
+// and [5] its duration, [6] the most iterations of any wave, [7] waves. A later launch of
+// the same solve combines with the earlier ones' values ([0] the first start, [1]/[2]/[4]/
+// [5] the last launch's, [6] the maximum).
+__device__ void reduce_wave_stats(const uint4* __restrict__ ws, int64_t n_waves, unsigned long long* lstats,
+                                  int first_batch) {
+    __shared__ unsigned long long s_start[kReduceBlock], s_deq[kReduceBlock], s_end[kReduceBlock];
+    __shared__ uint32_t s_it[kReduceBlock], s_dur[kReduceBlock], s_itmax[kReduceBlock];
+    unsigned long long st = ~0ull, dq = 0ull, en = 0ull;
+    uint32_t it = 0u, dur = 0u, itmax = 0u;
+    for (int64_t i = threadIdx.x; i < n_waves; i += kReduceBlock) {
+        const uint4 a = ws[2 * i], b = ws[2 * i + 1];
+        const unsigned long long t0 = (unsigned long long)a.y << 32 | a.x;
+        st = t0 < st ? t0 : st;
+        dq = t0 + a.z > dq ? t0 + a.z : dq;
+        if (t0 + a.w >= en) {
+            en = t0 + a.w;
+            it = b.x;
+            dur = a.w;
+        }
+        itmax = b.x > itmax ? b.x : itmax;
+    }
+    s_start[threadIdx.x] = st; s_deq[threadIdx.x] = dq; s_end[threadIdx.x] = en;
+    s_it[threadIdx.x] = it; s_dur[threadIdx.x] = dur; s_itmax[threadIdx.x] = itmax;
+    __syncthreads();
+    for (int h = kReduceBlock / 2; h > 0; h >>= 1) {
+        const int t = (int)threadIdx.x;
+        if (t < h) {
+            s_start[t] = s_start[t + h] < s_start[t] ? s_start[t + h] : s_start[t];
+            s_deq[t] = s_deq[t + h] > s_deq[t] ? s_deq[t + h] : s_deq[t];
+            if (s_end[t + h] > s_end[t]) {
+                s_end[t] = s_end[t + h];
+                s_it[t] = s_it[t + h];
+                s_dur[t] = s_dur[t + h];
+            }
+            s_itmax[t] = s_itmax[t + h] > s_itmax[t] ? s_itmax[t + h] : s_itmax[t];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        unsigned long long start = s_start[0], itm = s_itmax[0];
+        if (!first_batch) {
+            start = lstats[0] < start ? lstats[0] : start;
+            itm = lstats[6] > itm ? lstats[6] : itm;
+        }
+        lstats[0] = start;
+        lstats[1] = s_deq[0];
+        lstats[2] = s_end[0];
+        lstats[4] = s_it[0];
+        lstats[5] = s_dur[0];
+        lstats[6] = itm;
+        lstats[7] = (unsigned long long)n_waves;
+    }
+    __syncthreads();
+}
+
 // ns values per walk (multi-source solves): for each its sum and sum of
 // squares, then the steps -- rows of 2*ns+1 doubles. The summation order is
 // the same for every ns, so source k's sums do not depend on the other sources.
+// ctl (may be null): the walk launch's control words (wost_walk.h kCtlWords): workgroup 0
+// resets the queue head for the next launch and, with lstats, sums up the n_waves
+// launch statistics into lstats; every workgroup adds its longest walk to ctl[2]
+// (atomicMax), and the last one to finish moves it to lstats[3] and resets ctl[1..2].
 __global__ void __launch_bounds__(kReduceBlock)
 wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ steps,
                   const int64_t* __restrict__ begin, int64_t nblocks, int ns, double* __restrict__ out,
-                  unsigned long long* counter_reset) {
+                  unsigned long long* ctl, int64_t n_waves, unsigned long long* lstats, int first_batch) {
     __shared__ double s_sum[kReduceBlock], s_sq[kReduceBlock], s_st[kReduceBlock];
+    __shared__ uint32_t s_mx[kReduceBlock];
+    __shared__ int s_last;
     const int row = 2 * ns + 1;
-    if (counter_reset != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *counter_reset = 0ull;   // (a vector store)
+    if (ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ctl[0] = 0ull;   // (a vector store)
+    if (ctl != nullptr && lstats != nullptr && blockIdx.x == 0)
+        reduce_wave_stats(reinterpret_cast<const uint4*>(ctl + kCtlWords), n_waves, lstats, first_batch);
+    uint32_t mx_all = 0u;
     for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
         const int64_t lo = begin[b], hi = begin[b + 1];
         for (int k = 0; k < ns; ++k) {
@@ -220,7 +287,11 @@ wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ st
                 const double v = (double)val[i * ns + k];
                 s += v;
                 q += v * v;
-                if (k == 0) st += steps[i];
+                if (k == 0) {
+                    const uint32_t si = steps[i];
+                    st += si;
+                    mx_all = si > mx_all ? si : mx_all;
+                }
             }
             s_sum[threadIdx.x] = s;
             s_sq[threadIdx.x] = q;
@@ -242,15 +313,36 @@ wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ st
             __syncthreads();
         }
     }
+    if (ctl == nullptr || lstats == nullptr) return;
+    // the longest walk: one atomic per workgroup, then the last workgroup to finish moves it
+    s_mx[threadIdx.x] = mx_all;
+    __syncthreads();
+    for (int h = kReduceBlock / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h && s_mx[threadIdx.x + h] > s_mx[threadIdx.x]) s_mx[threadIdx.x] = s_mx[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicMax(ctl + 2, (unsigned long long)s_mx[0]);
+        __threadfence();
+        s_last = atomicAdd(ctl + 1, 1ull) == (unsigned long long)gridDim.x - 1ull;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x == 0) {
+        __threadfence();
+        const unsigned long long mx = atomicAdd(ctl + 2, 0ull);
+        lstats[3] = first_batch ? mx : (lstats[3] > mx ? lstats[3] : mx);
+        ctl[1] = 0ull;
+        ctl[2] = 0ull;
+    }
 }
 
 hipError_t launch_block_reduce(const float* val, const uint32_t* steps, const int64_t* begin,
-                               int64_t nblocks, int ns, double* out, unsigned long long* counter_reset,
-                               hipStream_t s) {
-    if (nblocks <= 0) return counter_reset ? hipMemsetAsync(counter_reset, 0, sizeof(unsigned long long), s)
-                                           : hipSuccess;
+                               int64_t nblocks, int ns, double* out, unsigned long long* ctl,
+                               hipStream_t s, int64_t n_waves, unsigned long long* lstats, int first_batch) {
+    if (nblocks <= 0) return ctl ? hipMemsetAsync(ctl, 0, sizeof(unsigned long long) * kCtlWords, s) : hipSuccess;
     const int grid = (int)(nblocks < 65536 ? nblocks : 65536);
-    wost_block_reduce<<<grid, kReduceBlock, 0, s>>>(val, steps, begin, nblocks, ns, out, counter_reset);
+    wost_block_reduce<<<grid, kReduceBlock, 0, s>>>(val, steps, begin, nblocks, ns, out, ctl, n_waves, lstats,
+                                                    first_batch);
     return hipGetLastError();
 }
 

@@ -164,6 +164,23 @@ void greens_sampler_nodes_jacobian(float* out, int n) {
     }
 }
 
+// I0 by its power series (every term positive: no cancellation, ~1 ulp) for x <= 30, where it
+// needs at most ~60 terms; i0_host's 4,096-panel quadrature otherwise. The sampler's
+// 65,537 density samples took 2.4 s of host time per handle through the quadrature -- the
+// whole cold start of a delta-tracking solve (bench.py "cold", profiles/r06_s1/).
+static double i0_series(double x) {
+    x = std::fabs(x);
+    if (x > 30.0) return i0_host(x);
+    const double q = 0.25 * x * x;
+    double term = 1.0, s = 1.0;
+    for (int k = 1; k < 200; ++k) {
+        term *= q / ((double)k * (double)k);
+        s += term;
+        if (term < 1e-17 * s) break;
+    }
+    return s;
+}
+
 void screened_sampler_nodes(float* out, int n, double sigma_bar) {
     const double a = 1e-6;
     const int J = 1 << 16;
@@ -175,7 +192,7 @@ void screened_sampler_nodes(float* out, int n, double sigma_bar) {
     std::vector<double> p(J + 1), C(J + 1);
     for (int j = 0; j <= J; ++j) {
         const double rho = a + j * h;
-        const double g = std::fabs((k0_host(rho * s) - ratio * i0_host(rho * s)) / (2.0 * kPi));
+        const double g = std::fabs((k0_host(rho * s) - ratio * i0_series(rho * s)) / (2.0 * kPi));
         p[j] = std::min(g, M);
     }
     C[0] = 0.0;

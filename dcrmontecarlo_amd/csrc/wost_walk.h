@@ -27,7 +27,8 @@ struct WalkArgs {
     const char* prog;            // DProgram + terms + factors (interpreted fields)
     float* out_val;              // [count] per-walk estimate
     uint32_t* out_steps;         // [count] per-walk step count
-    unsigned long long* counter; // work-queue head (zeroed before launch)
+    unsigned long long* counter; // the launch's control words (kCtlWords, zeroed before launch): [0] the
+                                 // work-queue head; the per-wave launch statistics after them
     int64_t wid_begin;           // global id of local walk 0
     int64_t count;               // walks in this launch
     int64_t walks_per_point;     // W: point of global walk g is g / W
@@ -88,12 +89,64 @@ struct WalkArgs {
     // the counter's dequeues start at queue_base = waves * chunk0 (>= count: none)
     int32_t chunk0;
     int64_t queue_base;
+    // adaptive dequeues (chunk_share > 0; walk_body's refill): a wave's dynamic dequeue takes
+    // at least the walks that keep the whole grid below ~4e7 dequeues per second at the
+    // grid's walk completion rate as this wave measures it -- the walks it has completed
+    // since it started, over the wall-clock ticks, times the grid's `waves` -- and at most
+    // chunk_share (count / (waves * 4): a quarter of a wave's even share). The launch shape
+    // is thus a function of this call alone, never of an earlier one.
+    uint32_t chunk_share;
+    uint32_t waves;
 };
+
+// The walk launch's control words (WalkArgs::counter): [0] the work-queue head, [1] the
+// block reduce's finished-workgroup count, [2] its longest walk, [3] unused; then per wave
+// two uint4 of launch statistics: {start tick low, high, last dequeue - start, end - start}
+// and {loop iterations, 0, 0, 0} (wave index as in the static chunks). Derived from the
+// queue's own pointer so that the walk loop keeps no extra pointer live.
+constexpr int kCtlWords = 4;
+WOST_HD constexpr size_t ctl_words(int64_t waves) { return (size_t)kCtlWords + 4 * (size_t)waves; }
 
 // words of one parked walk: global id (2), local index (2), x, y, dD, step | onB << 31,
 // phi, w, alpha(x), then the NS source totals
 WOST_HD constexpr int pool_fields(int ns) { return 11 + ns; }
 WOST_HD constexpr int pool_wg_words(int ns, int slots) { return 4 + 2 * pool_fields(ns) * slots; }
+
+// The GPU's constant-rate wall clock (s_memrealtime, 100 MHz on gfx950: hipDeviceAttribute-
+// WallClockRate), low 32 bits: differences are exact for launches shorter than ~42 s.
+__device__ __forceinline__ uint64_t wall_ticks64() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint64_t)__builtin_amdgcn_s_memrealtime();
+#else
+    return 0ull;
+#endif
+}
+__device__ __forceinline__ uint32_t wall_ticks() { return (uint32_t)wall_ticks64(); }
+// the grid's dequeue budget (~4e7 per second) per tick of the 100 MHz wall clock, inverted
+constexpr float kDequeuesPerTickInv = 1.0e8f / 4.0e7f;
+// The scan kernels' adaptive dequeues and launch statistics (walk_body). The segment-tree
+// kernels compile neither: their registers are full (96 VGPRs at 5 waves per SIMD, with
+// spills), their long walks take the host's 16-walk chunks, and the wave state they need
+// cost the C5 kernel ~4% (profiles/r06_ab/).
+#ifndef WOST_ADAPTIVE_DEQ
+#define WOST_ADAPTIVE_DEQ 1
+#endif
+#ifndef WOST_WAVE_STATS
+#define WOST_WAVE_STATS 1
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define WOST_KEEP_VGPR(v) __asm__ volatile("" : "+v"(v))
+#else
+#define WOST_KEEP_VGPR(v) ((void)0)
+#endif
+
+// Sum over the wave's lanes (every lane active), as a wave-uniform value.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
 
 // alpha at the query points with the walk kernel's own Fields policy (the same
 // function the walk would evaluate at its start point, hence the same bits).
@@ -861,6 +914,19 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     // wave-uniform work-queue state
     uint64_t c_next = 0, c_end = 0;
     bool exhausted = false;
+    // the wave's own measurements (adaptive dequeues, launch statistics): its start and
+    // last dequeue on the wall clock and its loop iterations (wave-uniform values kept in
+    // VGPRs: the SGPR file is full, and a uniform scalar here would spill into VGPR lanes
+    // through v_writelane / v_readlane inside the loop)
+    constexpr bool kAdaptive = WOST_ADAPTIVE_DEQ && !TREE;
+    constexpr bool kWaveStats = WOST_WAVE_STATS && !TREE;
+    uint32_t q_t0 = (kAdaptive || kWaveStats) ? wall_ticks() : 0u;
+    WOST_KEEP_VGPR(q_t0);
+    uint32_t q_tdeq = q_t0;   // (WOST_WAVE_STATS)
+    uint32_t q_iters = 0u;
+    WOST_KEEP_VGPR(q_iters);
+    uint32_t q_taken = 0u;   // walks this wave took from its static chunk and the queue (kAdaptive)
+    WOST_KEEP_VGPR(q_taken);
     {   // the wave's static first chunk (no atomic at the launch's start, when every wave
         // would hit the one counter at once)
         const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -996,8 +1062,22 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                     exhausted = true;
                     break;
                 }
+                // the dequeue's size: the host's (WalkArgs::chunk), raised (adaptive) to
+                // keep the grid below ~4e7 dequeues per second at the walk completion rate
+                // seen so far (cheap short walks: a counter dequeue per 64 walks would set
+                // the pace, 2.1e11 -> 7.0e10 walk-steps/s on Laplace), within chunk_share
+                uint32_t chunk = (uint32_t)A.chunk;
+                const uint32_t now = (kAdaptive || kWaveStats) ? wall_ticks() : 0u;
+                if (kAdaptive && A.chunk_share > 0u) {
+                    // the walks this wave completed: taken, less its lanes still walking
+                    const float done = (float)(q_taken - (64u - (uint32_t)__popcll(need)));
+                    // grid walks per second / 4e7 per second, at the 100 MHz wall clock
+                    const float lo = fminf((float)A.chunk_share, ceilf(done * (float)A.waves * kDequeuesPerTickInv /
+                                                                       ((float)(now - q_t0) + 1.0f)));
+                    chunk = (uint32_t)__builtin_amdgcn_readfirstlane((int)fmaxf(lo, (float)chunk));
+                }
                 unsigned long long c = 0;
-                if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)A.chunk);
+                if (lane == 0) c = atomicAdd(A.counter, (unsigned long long)chunk);
                 c += (unsigned long long)A.queue_base;
                 // lane 0's value as a scalar (every lane runs the refill): the queue
                 // state stays in SGPRs and the refill loop's control flow uniform
@@ -1007,8 +1087,12 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                     exhausted = true;
                     break;
                 }
+                if (kWaveStats) {
+                    q_tdeq = now;
+                    WOST_KEEP_VGPR(q_tdeq);
+                }
                 c_next = c;
-                c_end = c + (uint64_t)A.chunk;
+                c_end = c + (uint64_t)chunk;
                 if (c_end > (uint64_t)A.count) c_end = (uint64_t)A.count;
             }
             const uint64_t avail = c_end - c_next;
@@ -1055,6 +1139,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
                 active = true;
             }
             c_next += take;
+            if (kAdaptive) {
+                q_taken += take;
+                WOST_KEEP_VGPR(q_taken);
+            }
             need = __ballot(!active);
         }
         // the queue is exhausted: idle lanes take parked walks of either class, and the
@@ -1092,6 +1180,10 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
             pool_unlock(pool, lane, cnt[0], cnt[1]);
         }
         if (!__any(active)) break;
+        if (kWaveStats) {
+            q_iters += 1u;
+            WOST_KEEP_VGPR(q_iters);
+        }
         // a freshly refilled walk may already fail the while-condition (eps >= 1,
         // maxSteps == 0): it takes no step and is finished at the next iteration
         bool stepping = active && (k < A.max_steps) && (dD > A.eps);
@@ -1373,6 +1465,15 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         k += 1;                                                      // :291
         dD = dd;   // the loop tests the distance of the pre-step point (quirk Q7)
         WOST_PHASE("loop_head");
+    }
+    if (kWaveStats && lane == 0) {   // the launch statistics (wost_block_reduce sums them up)
+        uint4* const wave_stats = reinterpret_cast<uint4*>(A.counter + kCtlWords);
+        const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+        const uint64_t end = wall_ticks64();
+        const uint32_t dur = (uint32_t)end - q_t0;
+        const uint64_t start = end - dur;                   // the start's high word, from the end's
+        wave_stats[2 * wv] = uint4{(uint32_t)start, (uint32_t)(start >> 32), q_tdeq - q_t0, dur};
+        wave_stats[2 * wv + 1] = uint4{q_iters, 0u, 0u, 0u};
     }
 #if defined(WOST_TREE_ITER_STATS)
     // each lane's counters into the workgroup's study words after its pools (the host

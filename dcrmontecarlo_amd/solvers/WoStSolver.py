@@ -302,6 +302,22 @@ class WostSolver_2D:
         _lib.check(_lib.lib.wost_set_segment_tree(self._h, int(min_segments), int(leaf_segments)),
                    "wost_set_segment_tree")
 
+    def set_option(self, name: str, value):
+        """A kernel or launch option of this handle (include/wost.h wost_set_option: the
+        walk pools, LDS staging, work-queue chunks, tree hand-outs ...). None of them
+        changes a walk's value or step count; unknown names and bad values raise
+        ValueError, study-build-only names NotImplementedError."""
+        _lib.check(_lib.lib.wost_set_option(self._h, str(name).encode(), float(value)), f"set_option({name!r})")
+
+    def get_option(self, name: str) -> float:
+        v = ctypes.c_double(0.0)
+        _lib.check(_lib.lib.wost_get_option(self._h, str(name).encode(), ctypes.byref(v)), f"get_option({name!r})")
+        return float(v.value)
+
+    def options_report(self) -> dict:
+        """{"build": "product"|"study", "non_default": {name: value}} (wost_options_report)."""
+        return _lib.options_report(self._h)
+
     def num_blocks(self, n_points: int, nWalks: int) -> int:
         return int(_lib.lib.wost_num_blocks(int(n_points), int(nWalks)))
 

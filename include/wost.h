@@ -30,7 +30,7 @@ typedef unsigned long long uint64_t;
 extern "C" {
 #endif
 
-#define WOST_ABI_VERSION 4
+#define WOST_ABI_VERSION 5
 
 /* Most source fields one multi-source solve can score (wost_set_sources). */
 #define WOST_MAX_SOURCES 16
@@ -167,6 +167,28 @@ typedef struct {
     int32_t jit;                /* 1: field-specialised (hiprtc) walk kernel,
                                    0: precompiled kernel interpreting the fields */
     int32_t tree;               /* 1: Neumann queries through the segment tree */
+    /* the launch's shape -- a function of this call alone (never of an earlier solve):
+     * workgroups per CU and their threads, the static first chunk of walks per wave, the
+     * host's dequeue size and whether the waves then sized their dequeues from their own
+     * measured walks (wost_set_option "adaptive_chunk") */
+    int32_t blocks_per_cu;
+    int32_t block_threads;
+    int32_t chunk0;
+    int32_t chunk;
+    int32_t adaptive;
+    uint32_t max_walk_steps;    /* the longest walk's step count */
+    double jit_ms;              /* host time compiling the field-specialised kernel in this
+                                   solve (0 when the in-memory or disk cache had it) */
+    /* the device's wall clock over the solve's walk launches (s_memrealtime; the last
+     * launch for tail and last wave): first wave start -> last wave end; the last
+     * successful dequeue -> last wave end; the wave that ended last: its duration and
+     * loop iterations (one walk-step of at least one lane each); the most iterations of
+     * any wave */
+    double span_ms;
+    double tail_ms;
+    double last_wave_ms;
+    uint32_t last_wave_iters;
+    uint32_t max_wave_iters;
 } wost_timing;
 
 int wost_version(void);
@@ -385,8 +407,8 @@ int wost_dist_last_phases(double* ms);
 /* Walk kernels: by default libwost compiles a field-specialised walk kernel per
  * handle and kernel variant with hiprtc (cached in memory and in
  * $WOST_JIT_CACHE, default ~/.cache/wost) and falls back to the precompiled
- * interpreting kernel if that fails. enable = 0 forces the precompiled kernel
- * (also: environment WOST_JIT=0). Both give identical results. */
+ * interpreting kernel if that fails. enable = 0 forces the precompiled kernel.
+ * Both give identical results. */
 int wost_set_jit(wost_handle* h, int32_t enable);
 
 /* The walk direction's cos and sin (solvers/WoStSolver.py:230-232). The reference's
@@ -401,7 +423,8 @@ int wost_set_jit(wost_handle* h, int32_t enable);
  *                    curved boundary: C3's circle, C5's topography), fast otherwise
  *                    (Dirichlet-only problems and the DCR scenarios' straight top, whose
  *                    walks match the reference's either way).
- * Environment: WOST_TRIG = auto | exact | fast (the default of new handles). */
+ * (Study builds only: environment WOST_TRIG = auto | exact | fast, the default of new
+ * handles; the product library reads no environment variable that changes a kernel.) */
 enum wost_trig { WOST_TRIG_AUTO = 0, WOST_TRIG_EXACT = 1, WOST_TRIG_FAST = 2 };
 int wost_set_trig(wost_handle* h, int32_t mode);
 
@@ -419,9 +442,28 @@ int wost_set_fixed_step_check(wost_handle* h, int32_t enable);
  * PolylinesSimple.py:83-102, :134-197, which scan every segment) go through an
  * implicit 4-ary tree of oriented boxes and direction arcs with leaf_segments
  * (1..32) segments per leaf (0 keeps the current value), under both estimators (compat="fixed":
- * the nearest-crossing ray query). Results are bit-identical to the scans.
- * Environment: WOST_TREE_MIN_SEGMENTS, WOST_TREE_LEAF. */
+ * the nearest-crossing ray query). Results are bit-identical to the scans. */
 int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments);
+
+/* Kernel and launch options of a handle (no reference counterpart). Each selects HOW the
+ * walks run -- workgroup size, LDS staging, work-queue chunks, the segment tree's walk
+ * pools and hand-outs -- never what they compute: every walk's value and step count
+ * depend only on (seed, walk id), and the GPU tests check each option against the
+ * default walk for walk. Names (dcrmontecarlo_amd/csrc/wost_options.h): tree_pool,
+ * pool_near, pool_slots, pool_near_waves, pool_min_push, tree_lds, tree_lds_block,
+ * tree_share, tree_share_min, tree_share_descent, tree_batch, tree_qmargin, jit_waves,
+ * const_vertices, jit_slp, walk_block, fused_scan, refill_min, philox_ahead, chunk0,
+ * chunk_min, chunk_max, adaptive_chunk, grid_blocks_per_cu, lds_pad_bytes.
+ * WOST_ERR_INVALID_ARG for an unknown name or a value out of range; WOST_ERR_UNSUPPORTED
+ * for a study-build-only name (exp_flags, tree_iter_stats) in the product library. The
+ * product library reads no environment variable that changes a kernel or a result
+ * (study builds, build/libwost_study.so, seed options from the tools' A/B variables). */
+int wost_set_option(wost_handle* h, const char* name, double value);
+int wost_get_option(const wost_handle* h, const char* name, double* value);
+/* {"build": "product"|"study", "non_default": {name: value, ...}} as JSON (NUL-terminated,
+ * truncated to capacity - 1; *length = its full length). h may be NULL: the options a new
+ * handle would get. */
+int wost_options_report(const wost_handle* h, char* out, int64_t capacity, int64_t* length);
 
 /* HIP source of the field-specialised walk kernel wost_create would build for
  * this problem (host only, no device needed): for offline ISA study and for

@@ -148,31 +148,33 @@ def test_long_tree_with_wide_leaves_steps_down_its_staging(gpu_available):
     np.testing.assert_array_equal(tv.view(np.uint32), bv.view(np.uint32))
 
 
-@pytest.mark.parametrize("env", [{"WOST_POOL_SLOTS": "1", "WOST_POOL_NEAR_WAVES": "0"},
-                                 {"WOST_POOL_SLOTS": "3", "WOST_POOL_NEAR_WAVES": "16", "WOST_POOL_NEAR": "1"},
-                                 {"WOST_POOL_NEAR_WAVES": "1", "WOST_POOL_NEAR": "0.01"}, {}])
+def _with_options(s, opts):
+    for key, val in opts.items():
+        s.set_option(key, val)
+    return s
+
+
+@pytest.mark.parametrize("opts", [{"pool_slots": 1, "pool_near_waves": 0},
+                                  {"pool_slots": 3, "pool_near_waves": 16, "pool_near": 1.0},
+                                  {"pool_near_waves": 1, "pool_near": 0.01}, {}])
 @pytest.mark.parametrize("physical", [False, True])
-def test_c5_walk_pools_change_no_bits(gpu_available, monkeypatch, env, physical):
+def test_c5_walk_pools_change_no_bits(gpu_available, opts, physical):
     """The tree kernels' walk pools (wost_walk.h) move whole walks between a workgroup's
     waves: every walk's value and step count equal those without pools, for tiny pools
     (one slot: constant parking pressure), near classes that take every walk, narrow
-    near margins, and the defaults."""
+    near margins, and the defaults (wost_set_option)."""
     sc = _c5(physical=physical)
     pts = sc.points[::4][:64]
-    monkeypatch.setenv("WOST_TREE_POOL", "0")
-    s0 = sc.solver(device=0)
+    s0 = _with_options(sc.solver(device=0), {"tree_pool": 0})
     v0, k0 = s0.solve_walks(pts, nWalks=1024, maxSteps=sc.max_steps, eps=sc.eps, seed=31)
     assert s0.last_timing["tree"] == 1
-    monkeypatch.setenv("WOST_TREE_POOL", "1")
-    for key, val in env.items():
-        monkeypatch.setenv(key, val)
-    s1 = sc.solver(device=0)
+    s1 = _with_options(sc.solver(device=0), opts)
     v1, k1 = s1.solve_walks(pts, nWalks=1024, maxSteps=sc.max_steps, eps=sc.eps, seed=31)
     np.testing.assert_array_equal(np.asarray(k1), np.asarray(k0))
     np.testing.assert_array_equal(np.asarray(v1).view(np.uint32), np.asarray(v0).view(np.uint32))
 
 
-def test_c5_walk_pools_change_no_bits_with_many_sources(gpu_available, monkeypatch):
+def test_c5_walk_pools_change_no_bits_with_many_sources(gpu_available):
     """Multi-source walks (NS = 6: six totals travel with each parked walk) with one-slot
     pools equal the solve without pools, value for value and step for step."""
     from dcrmontecarlo_amd import survey
@@ -181,10 +183,8 @@ def test_c5_walk_pools_change_no_bits_with_many_sources(gpu_available, monkeypat
     srcs = [survey.dipole_source(sc.points[q], sc.points[q + 3], 0.5) for q in range(0, 60, 10)]
     pts = sc.points[::2][:32]
     out = []
-    for env in ({"WOST_TREE_POOL": "0"}, {"WOST_TREE_POOL": "1", "WOST_POOL_SLOTS": "1", "WOST_POOL_NEAR_WAVES": "0"}):
-        for key, val in env.items():
-            monkeypatch.setenv(key, val)
-        s = sc.solver(device=0)
+    for opts in ({"tree_pool": 0}, {"tree_pool": 1, "pool_slots": 1, "pool_near_waves": 0}):
+        s = _with_options(sc.solver(device=0), opts)
         out.append(s.solve_sources_walks(pts, srcs, nWalks=512, maxSteps=sc.max_steps, eps=sc.eps, seed=9))
     (v0, k0), (v1, k1) = out
     assert v0.shape == (len(srcs), len(pts), 512)
@@ -192,16 +192,14 @@ def test_c5_walk_pools_change_no_bits_with_many_sources(gpu_available, monkeypat
     np.testing.assert_array_equal(v1.view(np.uint32), v0.view(np.uint32))
 
 
-def test_c5_walk_pools_change_no_bits_in_walk_range_solves(gpu_available, monkeypatch):
+def test_c5_walk_pools_change_no_bits_in_walk_range_solves(gpu_available):
     """Walk-range solves (wost_solve_range, the multi-GPU shard unit: a launch's local
     walks map to point ranges) with one-slot pools equal those without pools."""
     sc = _c5()
     pts = sc.points[::8][:24]
     out = []
-    for env in ({"WOST_TREE_POOL": "0"}, {"WOST_TREE_POOL": "1", "WOST_POOL_SLOTS": "1", "WOST_POOL_NEAR_WAVES": "1"}):
-        for key, val in env.items():
-            monkeypatch.setenv(key, val)
-        s = sc.solver(device=0)
+    for opts in ({"tree_pool": 0}, {"tree_pool": 1, "pool_slots": 1, "pool_near_waves": 1}):
+        s = _with_options(sc.solver(device=0), opts)
         out.append(s.solve_range(pts, 8192, 4096, 8192, sc.max_steps, sc.eps, 21))
     assert out[0].shape[0] == len(pts)
     np.testing.assert_array_equal(out[1], out[0])
@@ -211,29 +209,21 @@ def test_c5_walk_pools_change_no_bits_in_walk_range_solves(gpu_available, monkey
 def test_c5_fused_bruteforce_scan_equals_separate_scans(gpu_available, name):
     """The brute-force scan kernel (set_segment_tree(-1)) runs both Neumann queries of a
     step in one pass with the per-vertex line filter (wost_device.h neumann_scan_both):
-    walk for walk the bits of the two separate full scans (WOST_EXP_FLAGS 2^28, the
+    walk for walk the bits of the two separate full scans (option fused_scan = 0, the
     round-4 kernel) and of the segment tree."""
-    import os
-
     from dcrmontecarlo_amd import scenarios as S
 
     sc = S.ALL[name](n_electrodes=64, n_walks=1)
     pts = sc.points[::2]
     runs = {}
-    for label, flags in (("fused", None), ("separate", str(1 << 28)), ("tree", None)):
-        old = os.environ.pop("WOST_EXP_FLAGS", None)
-        if flags:
-            os.environ["WOST_EXP_FLAGS"] = flags
-        try:
-            s = sc.solver(device=0)
-            if label != "tree":
-                s.set_segment_tree(-1)
-            runs[label] = s.solve_walks(pts, nWalks=512, maxSteps=sc.max_steps, eps=sc.eps, seed=29)
-            assert s.last_timing["tree"] == (1 if label == "tree" else 0)
-        finally:
-            os.environ.pop("WOST_EXP_FLAGS", None)
-            if old is not None:
-                os.environ["WOST_EXP_FLAGS"] = old
+    for label in ("fused", "separate", "tree"):
+        s = sc.solver(device=0)
+        if label != "tree":
+            s.set_segment_tree(-1)
+        if label == "separate":
+            s.set_option("fused_scan", 0)
+        runs[label] = s.solve_walks(pts, nWalks=512, maxSteps=sc.max_steps, eps=sc.eps, seed=29)
+        assert s.last_timing["tree"] == (1 if label == "tree" else 0)
     for label in ("separate", "tree"):
         np.testing.assert_array_equal(runs["fused"][1], runs[label][1], err_msg=label)
         np.testing.assert_array_equal(runs["fused"][0].view(np.uint32), runs[label][0].view(np.uint32), err_msg=label)

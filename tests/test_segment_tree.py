@@ -201,24 +201,27 @@ def test_gpu_tree_walks_match_scan_walks(gpu_available):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("knobs", [
-    {"WOST_TREE_LEAF": "1"}, {"WOST_TREE_LEAF": "32"},
-    {"WOST_JIT_TREE_SHARE": "0"}, {"WOST_JIT_TREE_SHARE": "64", "WOST_JIT_TREE_SHARE_MIN": "1"},
-    {"WOST_JIT_TREE_SHARE_DESCENT": "0", "WOST_JIT_TREE_BATCH": "1"},
-    {"WOST_JIT_TREE_BATCH": "2", "WOST_JIT_WAVES": "6"}, {"WOST_TREE_LDS": "0"}, {"WOST_TREE_LDS": "1"},
-    {"WOST_TREE_LDS": "0", "WOST_JIT_TREE_SHARE": "0"}])
-def test_gpu_cooperative_tree_variants_match_scan_walks(gpu_available, monkeypatch, knobs):
+    {"leaf": 1}, {"leaf": 32},
+    {"tree_share": 0}, {"tree_share": 64, "tree_share_min": 1},
+    {"tree_share_descent": 0, "tree_batch": 1},
+    {"tree_batch": 2, "jit_waves": 6}, {"tree_lds": 0}, {"tree_lds": 1},
+    {"tree_lds": 0, "tree_share": 0}])
+def test_gpu_cooperative_tree_variants_match_scan_walks(gpu_available, knobs):
     """The wave-cooperative tree queries (wost_walk.h: hand-outs of pending subtrees,
     batched record loads, records staged in LDS or read through L1/L2) under every
-    hand-out threshold, leaf size and load batch give the scan kernel's walks bit
-    for bit (the answers are order-independent
+    hand-out threshold, leaf size and load batch (wost_set_segment_tree, wost_set_option)
+    give the scan kernel's walks bit for bit (the answers are order-independent
     minima; only the visiting order and the lanes doing the visits change)."""
     sc = S.wenner_topography(n_electrodes=16, n_walks=512, n_segments=2000)
     s = sc.solver(device=0)
     s.set_segment_tree(-1)
     v0, st0 = s.solve_walks(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=21)
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)   # read when the handle is created / the kernel is generated
     s = sc.solver(device=0)
+    for k, v in knobs.items():
+        if k == "leaf":
+            s.set_segment_tree(64, v)
+        else:
+            s.set_option(k, v)
     v1, st1 = s.solve_walks(sc.points, nWalks=sc.n_walks, maxSteps=sc.max_steps, eps=sc.eps, seed=21)
     assert s.last_timing["tree"] == 1 and s.last_timing["jit"]
     np.testing.assert_array_equal(st1, st0)

@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--scan", action="store_true", help="force the full Neumann scans (no segment tree)")
     ap.add_argument("--cpu", action="store_true", help="also time the CPU oracle on a bounded sample")
     ap.add_argument("--cpu-seconds", type=float, default=3.0)
+    ap.add_argument("--opt", action="append", default=[], help="name=value: wost_set_option on every handle (A/B)")
     a = ap.parse_args()
     names = a.only.split(",") if a.only else list(SIZES)
     out = {}
@@ -75,11 +76,15 @@ def main():
             solver.set_fixed_step_check(False)
         if a.scan:
             solver.set_segment_tree(-1)
+        for kv in a.opt:
+            k, v = kv.split("=", 1)
+            solver.set_option(k, float(v))
         pts = sc.points[:npts]
         # warm-up at the full size: the JIT kernel, the tables and the per-walk workspace
         # (a smaller warm-up left the workspace's growth -- a hipFree/hipMalloc pair -- in
         # the first timed solve: round 4's erratic wall-vs-kernel gaps, tools/r05/host_overhead.py)
         solver.solve(pts, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=1)
+        t_first = dict(solver.last_timing)   # the fresh handle's first solve (its kernel time)
         best = None
         for r in range(a.reps):
             t0 = time.perf_counter()
@@ -99,6 +104,11 @@ def main():
         best["model_tflops"] = fps * best["steps_per_s_kernel"] / 1e12 if fps else float("nan")
         best["frac_fp32"] = best["model_tflops"] / perfmodel.FP32_PEAK_TFLOPS
         best["mean_steps"] = best["steps"] / (npts * W)
+        best["first_solve_steps_per_s_kernel"] = t_first["total_steps"] / (t_first["walk_kernel_ms"] * 1e-3)
+        best["first_over_best_kernel"] = t_first["walk_kernel_ms"] / best["kernel_ms"]
+        best["shape"] = {k: t_first.get(k) for k in ("grid_blocks", "blocks_per_cu", "chunk0", "chunk", "adaptive")}
+        best["tail_ms"] = t_first.get("tail_ms")
+        best["max_walk_steps"] = t_first.get("max_walk_steps")
         best["config"] = f"{npts} pts x {W} walks"
         out[name] = best
         cpu = ""
