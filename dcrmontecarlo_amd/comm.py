@@ -20,6 +20,7 @@ rank can read.
 from __future__ import annotations
 
 import ctypes
+import ipaddress
 import os
 import socket
 import socketserver
@@ -87,6 +88,25 @@ class _StoreServer(socketserver.ThreadingTCPServer):
     allow_reuse_address = True
 
 
+def _bind_address(host: str) -> str:
+    """Where rank 0's store listens: MASTER_ADDR itself (loopback for bench.py's own
+    launch), but every interface when the job spans nodes (WORLD_SIZE > LOCAL_WORLD_SIZE)
+    and MASTER_ADDR resolves to a loopback address on this node (the common 127.0.1.1
+    /etc/hosts entry), which peers on other nodes could not reach.
+    WOST_STORE_BIND overrides it."""
+    if os.environ.get("WOST_STORE_BIND") is not None:
+        return os.environ["WOST_STORE_BIND"]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world > local:
+        try:
+            if ipaddress.ip_address(socket.gethostbyname(host)).is_loopback:
+                return ""
+        except (OSError, ValueError):
+            pass
+    return host
+
+
 class SocketStore:
     """A minimal key-value store over TCP (standard library only) for the communicator's
     id: rank 0 hosts it (``is_master``), every rank -- rank 0 too -- is a client. ``get``
@@ -100,7 +120,7 @@ class SocketStore:
         self._srv = self._f = self._sock = None
         if is_master:
             self.kv, self.cond, self.closed = {}, threading.Condition(), False
-            self._srv = _StoreServer((host, int(port)), _StoreHandler)
+            self._srv = _StoreServer((_bind_address(host), int(port)), _StoreHandler)
             self._srv.store = self
             threading.Thread(target=self._srv.serve_forever, daemon=True).start()
         t0 = time.time()
@@ -174,7 +194,8 @@ class _FileStore:
         if st.st_uid != os.getuid() or (st.st_mode & 0o022):
             raise PermissionError(f"{d} is not a private directory of this user")
         self.dir, self.tag, self.rank, self.timeout, self.paths = d, tag, rank, timeout, []
-        self.not_before = _process_start_time() - 60.0
+        start = _process_start_time()
+        self.not_before = start - 60.0 if start is not None else 0.0   # (unknown start: the tag alone)
 
     def _path(self, key: str) -> str:
         safe = "".join(c if c.isalnum() else "_" for c in key)
@@ -211,14 +232,24 @@ class _FileStore:
         self.paths = []
 
 
-def _process_start_time() -> float:
-    """This process's start (wall clock, s); now if it cannot be read."""
+def _process_start_time():
+    """This process's start (wall clock, s): psutil, else /proc (the start in clock ticks
+    after boot plus the boot time), else None -- then no staleness test beyond the tag
+    (falling back to "now" made a late rank ignore a valid id file)."""
     try:
         import psutil
 
         return float(psutil.Process().create_time())
-    except Exception:   # psutil missing or refused: no staleness test beyond the tag
-        return time.time()
+    except Exception:
+        pass
+    try:
+        with open("/proc/self/stat") as f:
+            ticks = float(f.read().rsplit(")", 1)[1].split()[19])   # field 22: starttime
+        with open("/proc/stat") as f:
+            btime = next(float(l.split()[1]) for l in f if l.startswith("btime"))
+        return btime + ticks / os.sysconf("SC_CLK_TCK")
+    except Exception:
+        return None
 
 
 def _launch_tag() -> str:

@@ -1387,9 +1387,9 @@ WOST_HD ScanBoth neumann_scan_both(VP vin, int nv, float c1, float px, float py,
         float2 cs[kB];
 #pragma unroll
         for (int u = 0; u < kB; ++u) {
-            if constexpr (SCALAR) cs[u] = v[!kCheck || j0 + 1 + u < nv ? j0 + 1 + u : nv - 1];
-            else cs[u] = v[j0 + 1 + u];   // LDS (the staged copy): past the last vertex the staged
-                                          // data after it (or 0 beyond the allocation), unused
+            // (the last, partial batch clamps its index: no read past the polyline, in global
+            // memory or in the staged LDS copy; the clamped vertices are never used)
+            cs[u] = v[!kCheck || j0 + 1 + u < nv ? j0 + 1 + u : nv - 1];
         }
         const float2 b0 = b;
         const float cprev0 = cprev, lprev0 = lprev;

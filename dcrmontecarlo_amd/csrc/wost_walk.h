@@ -1247,7 +1247,11 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         float dnv = WOST_NAN;                                        // recorder: None without Neumann
         // a long polyline's brute-force scans in one pass (neumann_scan_both): the direction
         // first, the ray query's finish after r
+#if defined(WOST_ABL_NO_SILHOUETTE)   // (the ablation skips the fused scan, which draws the direction)
+        constexpr bool kFused = false;
+#else
         constexpr bool kFused = NEU && !TREE && !FIX && F::kFusedNeumann;
+#endif
         ScanBoth sb{};
         WOST_PHASE("silhouette");
         if (NEU) {

@@ -6,12 +6,11 @@ the CPU oracle (geometry/PolylinesSimple.py:25-49, :83-102, :134-197).
 * every step of recorded device walks: the Dirichlet distance and the Neumann
   silhouette distance the tree kernel used equal the oracle's full scans bit for
   bit (the tree must not change a single query);
-* device vs oracle on the same Philox streams (32 electrodes x 512 walks): the
-  walks that agree must be at least as many as those the oracle keeps against
-  ITSELF under a 1-ulp perturbation of the step direction, measured on the same
-  walks in the same test (their Q1 Neumann "hits" make C5 the most chaotic
-  scenario: ~87% self-agreement), less 2 points; and per-electrode means within
-  3 combined standard errors;
+* device vs oracle on the same Philox streams (32 electrodes x 512 walks): since
+  round 5's correctly rounded directions the device draws the oracle's walks, so
+  >= 99% of them must be identical (round 4's 0.82 fails), with the oracle's chaos
+  under a 1-ulp perturbation of the step direction (~87%, the Q1 Neumann "hits")
+  printed beside it; and per-electrode means within 1e-3 relative;
 * full size (256 electrodes x 10k walks): u(2f) = 2 u(f) bit for bit, and the tree
   kernel equals the brute-force scan kernel walk for walk on 64 electrodes x 256
   walks (~3.4M steps through both kernels);
@@ -77,11 +76,11 @@ def test_c5_device_matches_oracle(gpu_available):
     agree = lambda v, st: (st == os_) & (np.abs(v - ov) <= 1e-3 * np.abs(ov) + 1e-5 * scale)
     chaos = agree(pv, ps).mean()                   # the oracle against itself, 1 ulp apart
     device = agree(gv, gs).mean()
-    assert chaos > 0.5 and device >= chaos - 0.02, (device, chaos)
+    print(f"C5 device vs oracle: {device:.4f} of the walks identical (the oracle's 1-ulp chaos {chaos:.4f})")
+    assert chaos > 0.5 and device >= 0.99, (device, chaos)
     g = gv.astype(np.float64).reshape(len(pts), W)
     o = ov.astype(np.float64).reshape(len(pts), W)
-    se = np.sqrt(g.var(1, ddof=1) / W + o.var(1, ddof=1) / W)
-    assert np.all(np.abs(g.mean(1) - o.mean(1)) <= 3.0 * se + 1e-9 * scale)
+    np.testing.assert_allclose(g.mean(1), o.mean(1), rtol=1e-3, atol=1e-6 * scale)
 
 
 def test_c5_full_size_linearity_and_tree_equals_scan(gpu_available):

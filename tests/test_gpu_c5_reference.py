@@ -112,6 +112,105 @@ def test_c5_device_replays_reference_walks(gpu_available):
     np.testing.assert_allclose(m_g, m_r, rtol=1e-3, atol=1e-6 * np.abs(m_r).max())
 
 
+def _first_divergence(hist_w, z, a, n, rec):
+    """Where one diverged walk first leaves the reference's replayed path (tools/r05/
+    c5_divergence.py's classes): the first step j whose point or query distances differ,
+    classified by the transition j-1 -> j -- distance (the queries at j-1 differ),
+    direction (the source sample point at j-1 differs: direction or radius), collision
+    (same sample point, one walk moved to it and the other to the ray's point), ray (both
+    moved to the ray's point, which differs: the hit test) -- or `end` when every common
+    step agrees (step count or boundary term)."""
+    P, DD, DN, SP = rec
+    tol = lambda x, y: np.abs(x - y) <= 2e-3 * (1.0 + np.abs(y))
+    RP, Rd, Rn, RS = (z[k][a:a + n] for k in ("path_points", "path_dd", "path_dn", "src_points"))
+    GP, Gd, Gn, GS = P[:n], DD[:n], DN[:n], SP[:n]
+    dn_ok = (np.isnan(Gn) == np.isnan(Rn)) & np.where(np.isfinite(Rn), tol(Gn, np.nan_to_num(Rn)), True)
+    bad = ~(tol(GP, RP).all(1) & tol(Gd, Rd) & dn_ok)
+    if not bad.any():
+        return "end"
+    j = int(np.argmax(bad))
+    if j == 0:
+        return "start"
+    i = j - 1
+    if not (tol(Gd[i], Rd[i]) and dn_ok[i]):
+        return "distance"
+    if not tol(GS[i], RS[i]).all():
+        return "direction"
+    r_col, g_col = bool(np.all(RP[j] == RS[i])), bool(np.all(GP[j] == GS[i]))
+    return "collision" if r_col != g_col else ("sample" if r_col else "ray")
+
+
+@pytest.mark.parametrize("name", ["wenner_topography", "wenner_topography_physical"])
+def test_c5_replay_reference_histories(gpu_available, name):
+    """return_history on C5 against the reference's own history_dict on the same Philox
+    stream (tests/golden/replay_<name>.npz: 8 electrodes x 32 walks on the 10k-segment
+    topography, solvers/WoStSolver.py:184-309, structure :335-349): every step's point and
+    Dirichlet / silhouette distances, every source sample point and contribution and the
+    boundary term. A walk matches when its step count is the reference's and all its
+    records agree (2e-3 relative for points and distances, 1e-4 for contributions, as
+    tests/test_gpu_parity.py); the matching share must reach the oracle's own agreement
+    with the reference on these walks (its per-walk floor, measured here) less 0.02. Each
+    diverged walk's first divergent step is classified and printed."""
+    from collections import Counter
+
+    from oracle import oracle as O
+
+    from dcrmontecarlo_amd import scenarios as S
+    from dcrmontecarlo_amd.geometry import PolyLinesSimple
+    from dcrmontecarlo_amd.solvers import WostSolver_2D
+
+    z = golden(f"replay_{name}.npz")
+    sc = S.ALL[name](n_walks=1)
+    s = WostSolver_2D(PolyLinesSimple(z["dirichlet"]), sc.g, PolyLinesSimple(z["neumann"]), source=sc.f,
+                      alpha=sc.alpha)
+    W, pts = int(z["n_walks"]), z["points"]
+    kw = dict(maxSteps=int(z["max_steps"]), eps=float(z["eps"]), seed=int(z["seed"]))
+    u, hist = s.solve(pts, nWalks=W, return_history=True, **kw)
+    assert s.last_timing["tree"] == 1
+    walks = [w for i in range(len(pts)) for w in hist[i]]
+    rs = z["walk_steps"]
+    off = np.concatenate([[0], np.cumsum(rs)])
+    scale = max(float(np.abs(z["src_values"]).max()), 1e-30)
+    vscale = max(float(np.abs(z["walk_values"]).max()), 1e-30)
+    tol = lambda x, y: bool(np.all(np.abs(x - y) <= 2e-3 * (1.0 + np.abs(y))))
+    ok, kinds = [], Counter()
+    for j, w in enumerate(walks):
+        P = np.array([np.asarray(st["point"], np.float32) for st in w["path"]]).reshape(-1, 2)
+        DD = np.array([st["dirichlet_distance"] for st in w["path"]], np.float32)
+        DN = np.array([np.nan if st["neumann_distance"] is None else st["neumann_distance"] for st in w["path"]],
+                      np.float32)
+        src = [c for c in w["contributions"] if c["type"] == "source"]
+        assert len(src) == w["steps"] and len(w["path"]) == w["steps"]
+        SP = np.array([np.asarray(c["point"], np.float32) for c in src]).reshape(-1, 2)
+        SV = np.array([c["contribution"] for c in src], np.float32)
+        bnd = w["contributions"][-1]
+        assert bnd["type"] == "boundary" and bnd["step"] == w["steps"]
+        a, b = off[j], off[j + 1]
+        good = w["steps"] == rs[j]
+        if good:
+            rdn = z["path_dn"][a:b]
+            fin = np.isfinite(rdn)
+            good = (tol(P, z["path_points"][a:b]) and tol(DD, z["path_dd"][a:b])
+                    and np.array_equal(np.isnan(DN), np.isnan(rdn)) and tol(DN[fin], rdn[fin])
+                    and tol(SP, z["src_points"][a:b])
+                    and bool(np.all(np.abs(SV - z["src_values"][a:b]) <= 1e-4 * np.abs(z["src_values"][a:b])
+                                    + 1e-6 * scale))
+                    and tol(np.asarray(bnd["point"], np.float32), z["final_points"][j])
+                    and abs(bnd["contribution"] - z["boundary_values"][j])
+                    <= 1e-4 * abs(z["boundary_values"][j]) + 1e-6 * vscale)
+        if not good:
+            kinds[_first_divergence(w, z, a, min(int(rs[j]), int(w["steps"])), (P, DD, DN, SP))] += 1
+        ok.append(bool(good))
+    ok = np.array(ok)
+    pb = O.Problem(z["dirichlet"], z["neumann"], sc.g, sc.f, sc.sigma, sc.alpha)
+    pb = O.Problem(z["dirichlet"], z["neumann"], sc.g, sc.f, sc.sigma, sc.alpha, sigma_bar=pb.sigma_bar())
+    ov, os_ = pb.solve_walks(pts, W, kw["maxSteps"], kw["eps"], kw["seed"])
+    o_same, _ = c5_replay_agreement(ov, os_, z)
+    print(f"{name}: {ok.mean():.4f} of {len(ok)} walk histories match the reference's (the oracle's walks "
+          f"{o_same:.4f}); first divergence of the others: {dict(kinds)}")
+    assert ok.mean() >= o_same - 0.02, (ok.mean(), o_same, dict(kinds))
+
+
 def test_c5_device_replays_reference_rho_a(gpu_available):
     """G13: the reference's own C5 Wenner survey (setSourceTerm + _solveUnified on the
     Philox stream, physical conductivity and background, 16 quadripoles x both receivers x

@@ -528,6 +528,9 @@ REPLAYS = {
     # reference scans all 10k segments twice: ~1.6 ms per step)
     "wenner_topography": lambda: (S.wenner_topography(n_walks=1).points[[31, 63, 66, 100, 156, 189, 192, 224]], 32, 500,
                                   0.9, 77),
+    # round 6: the physical variant (no air term in the conductivity) at the same electrodes
+    "wenner_topography_physical": lambda: (
+        S.wenner_topography_physical(n_walks=1).points[[31, 63, 66, 100, 156, 189, 192, 224]], 32, 500, 0.9, 78),
 }
 
 
@@ -748,27 +751,29 @@ def tx_source(a, b, width=C5_WIDTH):
 
 
 def _c5_rho_worker(args):
-    field, q, k, e, W, seed_g, wid0, sigma_bar = args
+    name, field, q, k, e, W, seed_g, wid0, sigma_bar = args
     torch.set_num_threads(1)
     from dcrmontecarlo_amd import survey as SV  # noqa: F401 (the device survey's grouping, documented)
 
-    sc = S.wenner_topography_physical(n_walks=1)
-    spec = ref_scenarios()["wenner_topography_physical"]()
+    sc = S.ALL[name](n_walks=1)
+    spec = ref_scenarios()[name]()
     spec["f"] = tx_source(sc.points[q], sc.points[q + 3])
     if field == "background":
         spec["alpha"] = lambda p: C5_ALPHA_BG + 0.0 * p[0]
     pt = np.ascontiguousarray(sc.points[e:e + 1], np.float32)
-    v, s, sb = replay("wenner_topography_physical", pt, W, sc.max_steps, sc.eps, seed_g, wid0=wid0, spec=spec,
+    v, s, sb = replay(name, pt, W, sc.max_steps, sc.eps, seed_g, wid0=wid0, spec=spec,
                       values_only=True, sigma_bar=sigma_bar)
     return field, q, k, v, s, sb
 
 
-def gen_c5_rho_replay(walks, workers, n_quads=16):
+def gen_c5_rho_replay(walks, workers, n_quads=16, name="wenner_topography_physical"):
+    """name: the physical variant, or (round 6) the literal one the bench times
+    (notebook cell 17's conductivity with its air term; electrodes in 'air')."""
     import multiprocessing as mp
 
     from dcrmontecarlo_amd import survey as SV
 
-    sc = S.wenner_topography_physical(n_walks=1)
+    sc = S.ALL[name](n_walks=1)
     E = len(sc.points)
     quad = SV.wenner_quadripoles(E)
     qsel = np.unique(np.linspace(0, len(quad) - 1, n_quads).round().astype(np.int64))
@@ -777,7 +782,7 @@ def gen_c5_rho_replay(walks, workers, n_quads=16):
     for g, (j0, j1, t0, t1) in enumerate(batches):
         for j in range(j0, j1):
             group_of[j] = (g, j0)
-    spec = ref_scenarios()["wenner_topography_physical"]()
+    spec = ref_scenarios()[name]()
     with _quiet():
         sigma_bar = float(build_ref_solver(spec).sigma_bar)
     _NODES[sigma_bar] = screened_nodes(sigma_bar)     # forked workers inherit the sampler table
@@ -788,7 +793,7 @@ def gen_c5_rho_replay(walks, workers, n_quads=16):
             seed_g = SV.group_seed(C5_RHO_SEED, g)
             meta[i, k] = (e, g, j0, seed_g if seed_g < 2**63 else seed_g - 2**64)
             for field in ("model", "background"):
-                jobs.append((field, int(q), k, int(e), walks, seed_g, (int(e) - j0) * walks, sigma_bar))
+                jobs.append((name, field, int(q), k, int(e), walks, seed_g, (int(e) - j0) * walks, sigma_bar))
     vals = {f: np.zeros((len(qsel), 2, walks)) for f in ("model", "background")}
     steps = {f: np.zeros((len(qsel), 2, walks), np.int32) for f in ("model", "background")}
     row = {int(q): i for i, q in enumerate(qsel)}
@@ -801,7 +806,7 @@ def gen_c5_rho_replay(walks, workers, n_quads=16):
             if n % 8 == 7:
                 print(f"c5_rho_replay: {n + 1}/{len(jobs)} jobs, {time.time() - t0:.0f}s", flush=True)
     same = bool(np.array_equal(steps["model"], steps["background"]))
-    np.savez_compressed(os.path.join(OUT, "rho_replay_wenner_topography_physical.npz"), points=sc.points,
+    np.savez_compressed(os.path.join(OUT, f"rho_replay_{name}.npz"), points=sc.points,
                         quadripoles=quad[qsel], quad_index=qsel, receivers=meta[:, :, 0], groups=meta[:, :, 1],
                         group_j0=meta[:, :, 2], group_seeds=meta[:, :, 3].astype(np.int64).view(np.uint64),
                         survey_seed=np.uint64(C5_RHO_SEED), n_walks=np.int64(walks), max_steps=np.int64(sc.max_steps),
@@ -809,7 +814,7 @@ def gen_c5_rho_replay(walks, workers, n_quads=16):
                         sigma_bar=np.float64(sigma_bar), model_values=vals["model"],
                         background_values=vals["background"], model_steps=steps["model"],
                         background_steps=steps["background"], common_paths=np.bool_(same))
-    print("rho_replay_wenner_topography_physical.npz", f"{time.time() - t0:.0f}s", "common paths", same,
+    print(f"rho_replay_{name}.npz", f"{time.time() - t0:.0f}s", "common paths", same,
           "sigma_bar", sigma_bar, "mean steps", float(steps["model"].mean()))
 
 
@@ -821,6 +826,7 @@ def main():
     ap.add_argument("--rho-walks", type=int, default=400)
     ap.add_argument("--rho-replay-walks", type=int, default=256)
     ap.add_argument("--c5-rho-walks", type=int, default=64)
+    ap.add_argument("--c5-rho-quads", type=int, default=32)
     a = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     parts = set(a.only.split(","))
@@ -837,7 +843,7 @@ def main():
         gen_greens()
     if "sampler" in parts:
         gen_sampler_draws()
-    names = a.scenarios.split(",") if a.scenarios else [n for n in REPLAYS if n != "wenner_topography"]
+    names = a.scenarios.split(",") if a.scenarios else [n for n in REPLAYS if not n.startswith("wenner_topography")]
     if "replay" in parts:
         gen_replays(names)
     if "stats" in parts:
@@ -847,7 +853,9 @@ def main():
     if "rho_replay" in parts:
         gen_rho_replay(a.rho_replay_walks, a.stats_workers)
     if "c5_rho_replay" in parts:
-        gen_c5_rho_replay(a.c5_rho_walks, a.stats_workers)
+        gen_c5_rho_replay(a.c5_rho_walks, a.stats_workers, a.c5_rho_quads)
+    if "c5_rho_replay_literal" in parts:
+        gen_c5_rho_replay(a.c5_rho_walks, a.stats_workers, a.c5_rho_quads, name="wenner_topography")
 
 
 if __name__ == "__main__":
