@@ -437,6 +437,9 @@ def main():
         import tempfile
 
         os.environ["WOST_JIT_CACHE"] = tempfile.mkdtemp(prefix="wost_jit_bench_")
+        # and an empty code-object cache of ROCm's compiler library (comgr caches hiprtc's
+        # compiles on its own, so a kernel compiled by an earlier process would cost ~13 ms)
+        os.environ["AMD_COMGR_CACHE_DIR"] = os.path.join(os.environ["WOST_JIT_CACHE"], "comgr")
         library_check()
     world, rank, local = check_launch(args)
     if args.dry_launch:
@@ -877,14 +880,18 @@ def wenner_main(args, world, rank, local):
             out["rho_a_literal_timed_survey"] = rho_summary(res, sc.name)
         if E == 256 and not args.no_rho:
             # deterministic parity: the reference's own C5 Wenner survey replayed on the Philox
-            # stream (16 quadripoles x both receivers x 64 walks, physical model + background)
-            # against the device on the same walks
-            ref = survey.load_wenner_replay(os.path.join(REPO, "tests", "golden",
-                                                         "rho_replay_wenner_topography_physical.npz"))
-            if ref is not None:
-                cmp = survey.compare_wenner_replay(*survey.wenner_replay_walks(
-                    ref, survey.solver_replay_walks(pm, ph, ref)), ref)
-                out["rho_a"]["vs_reference_replay"] = cmp
+            # stream (32 quadripoles x both receivers x 64 walks, model + background) against
+            # the device on the same walks -- the physical survey the rho_a report comes from,
+            # and (round 6) the literal survey the bench times, on its own handles
+            legs = [("rho_a", "rho_replay_wenner_topography_physical.npz", pm, ph)]
+            if args.fields == "literal":
+                legs.append(("rho_a_literal_timed_survey", "rho_replay_wenner_topography.npz", sm, sh))
+            for key, fixture, mh, hh in legs:
+                ref = survey.load_wenner_replay(os.path.join(REPO, "tests", "golden", fixture))
+                if ref is not None and out.get(key) is not None and mh is not None:
+                    cmp = survey.compare_wenner_replay(*survey.wenner_replay_walks(
+                        ref, survey.solver_replay_walks(mh, hh, ref)), ref)
+                    out[key]["vs_reference_replay"] = cmp
         print(json.dumps(out), flush=True)
     if comm is not None:
         comm.barrier()

@@ -18,6 +18,7 @@ data:
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 
@@ -241,9 +242,10 @@ def compare_to_replay(vm: np.ndarray, vh: np.ndarray, sm: np.ndarray, sh: np.nda
 @dataclass
 class WennerReplay:
     """The reference's C5 Wenner survey replayed on libwost's Philox stream (tests/golden/
-    rho_replay_wenner_topography_physical.npz, tools/gen_fixtures.py --only c5_rho_replay):
+    rho_replay_wenner_topography_physical.npz and, round 6, rho_replay_wenner_topography.npz:
+    tools/gen_fixtures.py --only c5_rho_replay / c5_rho_replay_literal):
     setSourceTerm(transmitter q) + _solveUnified at both receivers (M, N) of each listed
-    quadripole, the physical conductivity and the alpha_bg background (the model's
+    quadripole, the physical (or literal) conductivity and the alpha_bg background (the model's
     sigma_bar), each receiver's walks carrying the ids and the seed they have in
     run_wenner_survey(seed=survey_seed): walk w of electrode e has id (e - j0) W + w in
     its group's launch, seed group_seed(survey_seed, g). Values and steps [Q, 2, W]."""
@@ -262,6 +264,7 @@ class WennerReplay:
     background_values: np.ndarray
     model_steps: np.ndarray
     background_steps: np.ndarray
+    source: str = "rho_replay_wenner_topography_physical.npz"   # the fixture file
 
 
 def load_wenner_replay(path: str) -> WennerReplay | None:
@@ -272,7 +275,7 @@ def load_wenner_replay(path: str) -> WennerReplay | None:
     return WennerReplay(z["points"], z["quadripoles"], z["receivers"], z["groups"], int(z["n_walks"]),
                         int(z["max_steps"]), float(z["eps"]), int(z["survey_seed"]), float(z["alpha_bg"]),
                         float(z["width"]), float(z["sigma_bar"]), z["model_values"], z["background_values"],
-                        z["model_steps"], z["background_steps"])
+                        z["model_steps"], z["background_steps"], os.path.basename(path))
 
 
 def wenner_replay_subset(ref: WennerReplay, idx) -> WennerReplay:
@@ -364,8 +367,7 @@ def compare_wenner_replay(vm, vh, sm, sh, ref: WennerReplay, k_sigma: float = 4.
     ok = np.abs(g - r) <= tol
     ok_a = np.abs(Ag - A) <= k_sigma * sig_a + e_m + 1e-5 * np.abs(A)
     clean = nd.sum(1) == 0
-    return {"fixture": "tests/golden/rho_replay_wenner_topography_physical.npz (reference setSourceTerm + "
-                       "_solveUnified on the Philox stream)",
+    return {"fixture": f"tests/golden/{ref.source} (reference setSourceTerm + _solveUnified on the Philox stream)",
             "quadripoles": int(len(r)), "walks_per_receiver": int(W),
             "walks_identical": float(1.0 - div.mean()),
             "steps_identical": float(np.mean(np.concatenate([(np.asarray(sm) == ref.model_steps).ravel(),

@@ -87,6 +87,9 @@ def _load():
     lib.orc_solve.restype = c_int32
     lib.orc_solve.argtypes = [POINTER(OrcProblem), fp, c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
                               c_uint64, c_int32, fp, POINTER(c_uint32)]
+    lib.orc_solve_history.restype = c_int32
+    lib.orc_solve_history.argtypes = [POINTER(OrcProblem), fp, c_int64, c_int64, c_int64, c_int64, c_int32,
+                                      c_float, c_uint64, c_int32, fp, POINTER(c_uint32), fp]
     return lib
 
 
@@ -162,6 +165,24 @@ class Problem:
         if rc != 0:
             raise ValueError(f"orc_solve failed ({rc})")
         return v, s
+
+    def solve_history(self, points, n_walks, max_steps, eps, seed, threads=0):
+        """(values f32 [walks], steps u32 [walks], records f32 [walks][max_steps][4]): every
+        walk's pre-step points and source sample points (return_history's path / source
+        contribution 'point', solvers/WoStSolver.py:218-266), steps 0 .. steps - 1."""
+        if threads <= 0:
+            threads = usable_cores()
+        pts = np.ascontiguousarray(points, np.float32).reshape(-1, 2)
+        n = pts.shape[0] * int(n_walks)
+        v = np.empty(n, np.float32)
+        s = np.empty(n, np.uint32)
+        rec = np.zeros((n, max(int(max_steps), 1), 4), np.float32)
+        rc = lib.orc_solve_history(ctypes.byref(self.p), _f(pts), pts.shape[0], int(n_walks), 0, n, int(max_steps),
+                                   float(eps), int(seed) & (2**64 - 1), int(threads), _f(v),
+                                   s.ctypes.data_as(POINTER(c_uint32)), _f(rec))
+        if rc != 0:
+            raise ValueError(f"orc_solve_history failed ({rc})")
+        return v, s, rec
 
     def solve(self, points, n_walks, max_steps, eps, seed, threads=0):
         """Per-point (mean, stderr, mean_steps) in float64."""

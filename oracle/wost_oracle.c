@@ -521,7 +521,11 @@ static float orc_gnorm(const orc_ctx* c, float r) {
     return c->inv_sb * (1.0f - inv);
 }
 
-static void orc_walk(const orc_ctx* c, uint64_t wid, float x0, float y0, float* value, uint32_t* steps) {
+/* rec (may be NULL): the walk's history as return_history records it (:218-266), 4 floats
+   per step: the pre-step point (path 'point') and the source sample point after the clip
+   (contributions 'point'; the ray's point without a source), max_steps records. */
+static void orc_walk(const orc_ctx* c, uint64_t wid, float x0, float y0, float* value, uint32_t* steps,
+                     float* rec) {
     const orc_problem* pb = c->pb;
     float px = x0, py = y0;
     int k = 0;
@@ -579,6 +583,10 @@ static void orc_walk(const orc_ctx* c, uint64_t wid, float x0, float y0, float* 
             }
             total = total + contrib;                                 /* :258 */
         }
+        if (rec) {                                                   /* :218-222, :261-266 */
+            rec[4 * k + 0] = px; rec[4 * k + 1] = py;
+            rec[4 * k + 2] = yx; rec[4 * k + 3] = yy;
+        }
         if (c->delta) {                                              /* :271-284 */
             float mu = orc_u01(rn[2]);
             gn = orc_gnorm(c, r);                                    /* :273 */
@@ -607,9 +615,10 @@ static void orc_walk(const orc_ctx* c, uint64_t wid, float x0, float y0, float* 
     *steps = (uint32_t)k;
 }
 
-int orc_solve(const orc_problem* pb, const float* points, int64_t n_points, int64_t W,
-              int64_t wid_begin, int64_t wid_end, int32_t max_steps, float eps, uint64_t seed,
-              int32_t threads, float* walk_values, uint32_t* walk_steps) {
+/* records (may be NULL): [wid_end - wid_begin][max_steps][4] floats of orc_walk's rec */
+int orc_solve_history(const orc_problem* pb, const float* points, int64_t n_points, int64_t W,
+                      int64_t wid_begin, int64_t wid_end, int32_t max_steps, float eps, uint64_t seed,
+                      int32_t threads, float* walk_values, uint32_t* walk_steps, float* records) {
     if (!pb || !pb->dxy || pb->nd < 2 || W <= 0 || wid_begin < 0 || wid_end < wid_begin ||
         wid_end > n_points * W)
         return -1;
@@ -652,7 +661,15 @@ int orc_solve(const orc_problem* pb, const float* points, int64_t n_points, int6
     for (int64_t i = 0; i < n; ++i) {
         uint64_t wid = (uint64_t)(wid_begin + i);
         int64_t p = (int64_t)(wid / (uint64_t)W);
-        orc_walk(&c, wid, points[2 * p], points[2 * p + 1], &walk_values[i], &walk_steps[i]);
+        orc_walk(&c, wid, points[2 * p], points[2 * p + 1], &walk_values[i], &walk_steps[i],
+                 records ? records + (size_t)i * (size_t)max_steps * 4u : NULL);
     }
     return 0;
+}
+
+int orc_solve(const orc_problem* pb, const float* points, int64_t n_points, int64_t W,
+              int64_t wid_begin, int64_t wid_end, int32_t max_steps, float eps, uint64_t seed,
+              int32_t threads, float* walk_values, uint32_t* walk_steps) {
+    return orc_solve_history(pb, points, n_points, W, wid_begin, wid_end, max_steps, eps, seed, threads,
+                             walk_values, walk_steps, NULL);
 }

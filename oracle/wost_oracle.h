@@ -81,6 +81,12 @@ void orc_philox(uint32_t ctr[4], uint32_t k0, uint32_t k1, uint32_t out[4]);
 int orc_solve(const orc_problem* pb, const float* points, int64_t n_points, int64_t W,
               int64_t wid_begin, int64_t wid_end, int32_t max_steps, float eps, uint64_t seed,
               int32_t threads, float* walk_values, uint32_t* walk_steps);
+/* orc_solve with return_history's records (:218-266): records[walk][max_steps][4] =
+ * the pre-step point and the source sample point after the clip (the ray's point
+ * without a source), for steps 0 .. walk_steps - 1 (records may be NULL). */
+int orc_solve_history(const orc_problem* pb, const float* points, int64_t n_points, int64_t W,
+                      int64_t wid_begin, int64_t wid_end, int32_t max_steps, float eps, uint64_t seed,
+                      int32_t threads, float* walk_values, uint32_t* walk_steps, float* records);
 
 #ifdef __cplusplus
 }

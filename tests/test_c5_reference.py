@@ -188,16 +188,27 @@ def oracle_wenner_walks(ref, sc):
     return solve_walks
 
 
-def test_c5_rho_replay_fixture_is_the_survey_layout():
-    """G13 (rho_replay_wenner_topography_physical.npz): the receivers are the quadripoles'
-    M and N, their groups and seeds those of survey.run_wenner_survey, model and
-    background walks share their paths (common random numbers)."""
+# the oracle's share of the reference's C5 Wenner walks it reproduces on the whole fixture
+# (32 quadripoles x both receivers x 64 walks x model + background), measured with
+# survey.compare_wenner_replay over oracle_wenner_walks (round 6; ~6 min of CPU for the
+# literal survey's 204-step walks, so the CPU test below checks 4 of the quadripoles):
+# the device's floor in tests/test_gpu_c5_reference.py
+ORACLE_RHO_IDENTICAL = {"wenner_topography": 0.918, "wenner_topography_physical": 0.982}
+
+
+@pytest.mark.parametrize("name", ["wenner_topography", "wenner_topography_physical"])
+def test_c5_rho_replay_fixture_is_the_survey_layout(name):
+    """G13 (rho_replay_<name>.npz: the physical survey, and since round 6 the literal one
+    the bench times): the receivers are the quadripoles' M and N, their groups and seeds
+    those of survey.run_wenner_survey, model and background walks share their paths
+    (common random numbers), 32 quadripoles."""
     from dcrmontecarlo_amd import scenarios as S
     from dcrmontecarlo_amd import survey as SV
 
-    z = golden("rho_replay_wenner_topography_physical.npz")
-    ref = SV.load_wenner_replay(os.path.join(HERE, "golden", "rho_replay_wenner_topography_physical.npz"))
-    sc = S.wenner_topography_physical(n_walks=1)
+    z = golden(f"rho_replay_{name}.npz")
+    ref = SV.load_wenner_replay(os.path.join(HERE, "golden", f"rho_replay_{name}.npz"))
+    assert ref.source == f"rho_replay_{name}.npz" and len(ref.quadripoles) == 32
+    sc = S.ALL[name](n_walks=1)
     np.testing.assert_array_equal(ref.points, sc.points)
     np.testing.assert_array_equal(ref.receivers, ref.quadripoles[:, 1:3])
     batches = list(SV.wenner_batches(len(sc.points)))
@@ -208,19 +219,21 @@ def test_c5_rho_replay_fixture_is_the_survey_layout():
             assert j0 <= ref.receivers[i, k] < j1 and t0 <= ref.quadripoles[i, 0] < t1
             assert int(z["group_seeds"][i, k]) == SV.group_seed(ref.survey_seed, g)
     assert bool(z["common_paths"]) and np.array_equal(ref.model_steps, ref.background_steps)
-    assert ref.sigma_bar == pytest.approx(float(golden("fields_wenner_topography_physical.npz")["sigma_bar"]), rel=1e-12)
+    assert ref.sigma_bar == pytest.approx(float(golden(f"fields_{name}.npz")["sigma_bar"]), rel=1e-12)
 
 
-def test_oracle_replays_reference_c5_rho_a():
-    """The oracle on the reference's C5 Wenner walks (4 of the 16 quadripoles): >= 96% of
-    the walks identical, and every quadripole's dV and rho_a within the bound the
-    diverged walks allow (survey.compare_wenner_replay)."""
+@pytest.mark.parametrize("name", ["wenner_topography", "wenner_topography_physical"])
+def test_oracle_replays_reference_c5_rho_a(name):
+    """The oracle on the reference's C5 Wenner walks (4 of the 32 quadripoles): the walks
+    identical as often as on the whole fixture (ORACLE_RHO_IDENTICAL) less 0.03, and every
+    quadripole's dV and rho_a within the bound the diverged walks allow
+    (survey.compare_wenner_replay)."""
     from dcrmontecarlo_amd import scenarios as S
     from dcrmontecarlo_amd import survey as SV
 
-    ref = SV.load_wenner_replay(os.path.join(HERE, "golden", "rho_replay_wenner_topography_physical.npz"))
-    ref = SV.wenner_replay_subset(ref, [1, 6, 9, 13])
-    sc = S.wenner_topography_physical(n_walks=1)
+    ref = SV.load_wenner_replay(os.path.join(HERE, "golden", f"rho_replay_{name}.npz"))
+    ref = SV.wenner_replay_subset(ref, [3, 12, 19, 28])
+    sc = S.ALL[name](n_walks=1)
     out = SV.compare_wenner_replay(*SV.wenner_replay_walks(ref, oracle_wenner_walks(ref, sc)), ref)
-    assert out["walks_identical"] >= 0.96, out["walks_identical"]
+    assert out["walks_identical"] >= ORACLE_RHO_IDENTICAL[name] - 0.03, out["walks_identical"]
     assert out["all_within_tolerance"], out

@@ -140,17 +140,43 @@ def _first_divergence(hist_w, z, a, n, rec):
     return "collision" if r_col != g_col else ("sample" if r_col else "ray")
 
 
+def _history_agreement(P, SP, steps, z, tol_rel=2e-3):
+    """(share of the reference's step records a history reproduces before its first
+    divergence, share of walks whose whole history agrees): a walk's records agree while
+    its pre-step point and source sample point stay within tol_rel of the reference's.
+    P, SP: per walk [steps, 2] arrays."""
+    rs = z["walk_steps"]
+    ro = np.concatenate([[0], np.cumsum(rs)])
+    tol = lambda x, y: np.all(np.abs(x - y) <= tol_rel * (1.0 + np.abs(y)), axis=1)
+    pre = full = 0
+    for w in range(len(rs)):
+        n = min(int(rs[w]), int(steps[w]))
+        ok = tol(P[w][:n], z["path_points"][ro[w]:ro[w] + n]) & tol(SP[w][:n], z["src_points"][ro[w]:ro[w] + n])
+        j = n if ok.all() else int(np.argmin(ok))
+        pre += j
+        full += int(j == rs[w] and steps[w] == rs[w])
+    return pre / float(ro[-1]), full / float(len(rs))
+
+
 @pytest.mark.parametrize("name", ["wenner_topography", "wenner_topography_physical"])
 def test_c5_replay_reference_histories(gpu_available, name):
     """return_history on C5 against the reference's own history_dict on the same Philox
     stream (tests/golden/replay_<name>.npz: 8 electrodes x 32 walks on the 10k-segment
-    topography, solvers/WoStSolver.py:184-309, structure :335-349): every step's point and
-    Dirichlet / silhouette distances, every source sample point and contribution and the
-    boundary term. A walk matches when its step count is the reference's and all its
-    records agree (2e-3 relative for points and distances, 1e-4 for contributions, as
-    tests/test_gpu_parity.py); the matching share must reach the oracle's own agreement
-    with the reference on these walks (its per-walk floor, measured here) less 0.02. Each
-    diverged walk's first divergent step is classified and printed."""
+    topography; solvers/WoStSolver.py:184-309, structure :335-349).
+
+    C5's walks are chaotic: the reference's own last-ulp arithmetic (torch's MKL cos/sin,
+    its 10k-element reductions) sends a walk off its replayed path at some step, and the
+    divergence grows -- so the walk values agree far more often (0.93 literal, of which
+    more than half are 0: weights that underflow in the literal fields' 'air') than whole
+    histories do (0.34 literal, 0.82 physical). The floor is therefore the oracle's OWN
+    history agreement with the reference on the same walks, measured here with its
+    recorder (oracle orc_solve_history): the device's histories must reproduce as many of
+    the reference's step records before their first divergence, and as many whole walks,
+    as the oracle's, less 0.02; and equal the oracle's histories on >= 99% of the walks
+    (1e-5 relative). Each walk's records have the reference's structure; the walks whose
+    whole path agrees carry the reference's source contributions (1e-3 relative: the
+    weights' float rounding accumulates over ~200 steps) and boundary terms; the first
+    divergence of the other walks is classified and printed."""
     from collections import Counter
 
     from oracle import oracle as O
@@ -170,67 +196,89 @@ def test_c5_replay_reference_histories(gpu_available, name):
     walks = [w for i in range(len(pts)) for w in hist[i]]
     rs = z["walk_steps"]
     off = np.concatenate([[0], np.cumsum(rs)])
-    scale = max(float(np.abs(z["src_values"]).max()), 1e-30)
-    vscale = max(float(np.abs(z["walk_values"]).max()), 1e-30)
-    tol = lambda x, y: bool(np.all(np.abs(x - y) <= 2e-3 * (1.0 + np.abs(y))))
-    ok, kinds = [], Counter()
-    for j, w in enumerate(walks):
-        P = np.array([np.asarray(st["point"], np.float32) for st in w["path"]]).reshape(-1, 2)
-        DD = np.array([st["dirichlet_distance"] for st in w["path"]], np.float32)
-        DN = np.array([np.nan if st["neumann_distance"] is None else st["neumann_distance"] for st in w["path"]],
-                      np.float32)
+    P, DD, DN, SP, SV, steps = [], [], [], [], [], []
+    for w in walks:   # the reference's structure (:197-309)
+        assert len(w["path"]) == w["steps"]
         src = [c for c in w["contributions"] if c["type"] == "source"]
-        assert len(src) == w["steps"] and len(w["path"]) == w["steps"]
-        SP = np.array([np.asarray(c["point"], np.float32) for c in src]).reshape(-1, 2)
-        SV = np.array([c["contribution"] for c in src], np.float32)
+        assert len(src) == w["steps"] and [c["step"] for c in src] == list(range(w["steps"]))
         bnd = w["contributions"][-1]
         assert bnd["type"] == "boundary" and bnd["step"] == w["steps"]
-        a, b = off[j], off[j + 1]
-        good = w["steps"] == rs[j]
-        if good:
-            rdn = z["path_dn"][a:b]
-            fin = np.isfinite(rdn)
-            good = (tol(P, z["path_points"][a:b]) and tol(DD, z["path_dd"][a:b])
-                    and np.array_equal(np.isnan(DN), np.isnan(rdn)) and tol(DN[fin], rdn[fin])
-                    and tol(SP, z["src_points"][a:b])
-                    and bool(np.all(np.abs(SV - z["src_values"][a:b]) <= 1e-4 * np.abs(z["src_values"][a:b])
-                                    + 1e-6 * scale))
-                    and tol(np.asarray(bnd["point"], np.float32), z["final_points"][j])
-                    and abs(bnd["contribution"] - z["boundary_values"][j])
-                    <= 1e-4 * abs(z["boundary_values"][j]) + 1e-6 * vscale)
-        if not good:
-            kinds[_first_divergence(w, z, a, min(int(rs[j]), int(w["steps"])), (P, DD, DN, SP))] += 1
-        ok.append(bool(good))
-    ok = np.array(ok)
+        P.append(np.array([np.asarray(st["point"], np.float32) for st in w["path"]]).reshape(-1, 2))
+        DD.append(np.array([st["dirichlet_distance"] for st in w["path"]], np.float32))
+        DN.append(np.array([np.nan if st["neumann_distance"] is None else st["neumann_distance"]
+                            for st in w["path"]], np.float32))
+        SP.append(np.array([np.asarray(c["point"], np.float32) for c in src]).reshape(-1, 2))
+        SV.append(np.array([c["contribution"] for c in src], np.float32))
+        steps.append(w["steps"])
+    steps = np.array(steps)
     pb = O.Problem(z["dirichlet"], z["neumann"], sc.g, sc.f, sc.sigma, sc.alpha)
     pb = O.Problem(z["dirichlet"], z["neumann"], sc.g, sc.f, sc.sigma, sc.alpha, sigma_bar=pb.sigma_bar())
-    ov, os_ = pb.solve_walks(pts, W, kw["maxSteps"], kw["eps"], kw["seed"])
-    o_same, _ = c5_replay_agreement(ov, os_, z)
-    print(f"{name}: {ok.mean():.4f} of {len(ok)} walk histories match the reference's (the oracle's walks "
-          f"{o_same:.4f}); first divergence of the others: {dict(kinds)}")
-    assert ok.mean() >= o_same - 0.02, (ok.mean(), o_same, dict(kinds))
+    ov, os_, orec = pb.solve_history(pts, W, kw["maxSteps"], kw["eps"], kw["seed"])
+    # the device's histories are the oracle's
+    dev_oracle = np.mean([steps[w] == os_[w] and np.allclose(P[w], orec[w, :steps[w], :2], rtol=1e-5, atol=1e-5)
+                          and np.allclose(SP[w], orec[w, :steps[w], 2:], rtol=1e-5, atol=1e-5)
+                          for w in range(len(walks))])
+    d_pre, d_full = _history_agreement(P, SP, steps, z)
+    o_pre, o_full = _history_agreement([orec[w, :os_[w], :2] for w in range(len(os_))],
+                                       [orec[w, :os_[w], 2:] for w in range(len(os_))], os_, z)
+    # the walks whose whole path agrees: their contributions and boundary terms
+    tol = lambda x, y: bool(np.all(np.abs(x - y) <= 2e-3 * (1.0 + np.abs(y))))
+    scale = max(float(np.abs(z["src_values"]).max()), 1e-30)
+    vscale = max(float(np.abs(z["walk_values"]).max()), 1e-30)
+    kinds, bad_terms = Counter(), 0
+    for j, w in enumerate(walks):
+        a, b = off[j], off[j + 1]
+        n = min(int(rs[j]), int(steps[j]))
+        whole = (steps[j] == rs[j] and tol(P[j], z["path_points"][a:b]) and tol(SP[j], z["src_points"][a:b])
+                 and tol(np.asarray(w["contributions"][-1]["point"], np.float32), z["final_points"][j]))
+        if not whole:
+            kinds[_first_divergence(w, z, a, n, (P[j], DD[j], DN[j], SP[j]))] += 1
+            continue
+        rdn = z["path_dn"][a:b]
+        fin = np.isfinite(rdn)
+        # a distance moves no more than its point (1-Lipschitz): the points' own slack added
+        slack = np.abs(P[j] - z["path_points"][a:b]).sum(1)
+        ok = (bool(np.all(np.abs(DD[j] - z["path_dd"][a:b]) <= 2e-3 * (1.0 + np.abs(z["path_dd"][a:b])) + slack))
+              and np.array_equal(np.isnan(DN[j]), np.isnan(rdn))
+              and bool(np.all(np.abs(DN[j][fin] - rdn[fin]) <= 2e-3 * (1.0 + np.abs(rdn[fin])) + slack[fin]))
+              and bool(np.all(np.abs(SV[j] - z["src_values"][a:b]) <= 1e-3 * np.abs(z["src_values"][a:b]) + 1e-6 * scale))
+              and abs(w["contributions"][-1]["contribution"] - z["boundary_values"][j])
+              <= 1e-3 * abs(z["boundary_values"][j]) + 1e-6 * vscale)
+        bad_terms += int(not ok)
+    print(f"{name}: device histories = the oracle's on {dev_oracle:.4f} of the walks; the reference's step records "
+          f"reproduced before the first divergence: device {d_pre:.4f}, oracle {o_pre:.4f}; whole histories: device "
+          f"{d_full:.4f}, oracle {o_full:.4f}; first divergence of the others: {dict(kinds)}; whole-path walks with "
+          f"other terms: {bad_terms}")
+    assert dev_oracle >= 0.99, dev_oracle
+    assert d_pre >= o_pre - 0.02 and d_full >= o_full - 0.02, (d_pre, o_pre, d_full, o_full)
+    assert bad_terms <= max(1, int(0.02 * len(walks))), bad_terms
 
 
-def test_c5_device_replays_reference_rho_a(gpu_available):
+@pytest.mark.parametrize("name", ["wenner_topography", "wenner_topography_physical"])
+def test_c5_device_replays_reference_rho_a(gpu_available, name):
     """G13: the reference's own C5 Wenner survey (setSourceTerm + _solveUnified on the
-    Philox stream, physical conductivity and background, 16 quadripoles x both receivers x
-    64 walks; tests/golden/rho_replay_wenner_topography_physical.npz) against the device on
-    the same walks, launched per electrode group as run_wenner_survey launches them: the
-    walks identical at least as often as the oracle's (0.980 on all 16 quadripoles) less
-    0.02, and every quadripole's dV and rho_a within the bound its diverged walks allow
-    (survey.compare_wenner_replay)."""
+    Philox stream, model + homogeneous background, 32 quadripoles x both receivers x 64
+    walks; tests/golden/rho_replay_<name>.npz -- the physical survey, and since round 6 the
+    literal one the bench times) against the device on the same walks, launched per
+    electrode group as run_wenner_survey launches them: the walks identical at least as
+    often as the oracle's on the whole fixture (test_c5_reference.ORACLE_RHO_IDENTICAL:
+    0.918 literal, 0.982 physical) less 0.02, and every quadripole's dV and rho_a within
+    the bound its diverged walks allow (survey.compare_wenner_replay)."""
     import os
+
+    from test_c5_reference import ORACLE_RHO_IDENTICAL
 
     from dcrmontecarlo_amd import scenarios as S
     from dcrmontecarlo_amd import survey as SV
 
     ref = SV.load_wenner_replay(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
-                                             "rho_replay_wenner_topography_physical.npz"))
-    sc = S.wenner_topography_physical(n_walks=1)
+                                             f"rho_replay_{name}.npz"))
+    sc = S.ALL[name](n_walks=1)
     sm = sc.solver(device=0)
     sh = SV.homogeneous_solver(sc, ref.alpha_bg, sm, device=0)
     out = SV.compare_wenner_replay(*SV.wenner_replay_walks(ref, SV.solver_replay_walks(sm, sh, ref)), ref)
-    print("C5 rho_a replay: walks identical", out["walks_identical"], "diverged per quadripole",
-          out["diverged_walks"], "dV max d/sigma_chaos", out["dv_model"]["max_d_over_sigma_chaos"])
-    assert out["walks_identical"] >= 0.96, out["walks_identical"]
+    print(f"C5 {name} rho_a replay: walks identical", out["walks_identical"], "(oracle", ORACLE_RHO_IDENTICAL[name],
+          ") diverged per quadripole", out["diverged_walks"], "rho_a max d/sigma_chaos",
+          out["rho_a"]["max_d_over_sigma_chaos"])
+    assert out["walks_identical"] >= ORACLE_RHO_IDENTICAL[name] - 0.02, out["walks_identical"]
     assert out["all_within_tolerance"], out
