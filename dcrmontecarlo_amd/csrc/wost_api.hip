@@ -1406,11 +1406,26 @@ int wost_set_sources(wost_handle* h, const wost_field* const* sources, int32_t n
 }
 
 
-int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int64_t* length) {
+int wost_kernel_source_sources(const wost_problem* pb, const wost_field* const* sources, int32_t n_sources,
+                               char* out, int64_t capacity, int64_t* length) {
     if (!pb || !length) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    if (n_sources < 0 || n_sources > WOST_MAX_SOURCES || (n_sources > 0 && !sources))
+        return fail(WOST_ERR_INVALID_ARG, "need 0..%d sources", WOST_MAX_SOURCES);
     wost_handle* h = nullptr;
     int rc = create_host(pb, &h);
     if (rc != WOST_OK) return rc;
+    int ns = 1;
+    if (n_sources >= 1) {   // wost_set_sources' fields, without a device
+        for (int k = 0; k < n_sources; ++k) {
+            HostField hf;
+            if (!sources[k] || (rc = convert_field(sources[k], hf, "source")) != WOST_OK) {
+                delete h;
+                return rc != WOST_OK ? rc : fail(WOST_ERR_INVALID_ARG, "source %d is NULL", k);
+            }
+            h->fields[k == 0 ? SLOT_F : SLOT_EXTRA + k - 1] = hf;
+        }
+        ns = n_sources;
+    }
     build_program(h->fields, h->sigma_bar, h->prog);
     const int mode = walk_mode(h);
     // no device here: the segment angles of a compiled-in Neumann polyline come from the
@@ -1433,7 +1448,7 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
     }
 #endif
     const std::string src = jit_generate(h->opt, mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(), h->dverts.data(),
-                                         (int)(h->dverts.size() / 2), h->nverts.data(), nn, false, 1, block,
+                                         (int)(h->dverts.size() / 2), h->nverts.data(), nn, false, ns, block,
                                          phi.empty() ? nullptr : phi.data(), false, stage, exact_trig_of(h));
     delete h;
     *length = (int64_t)src.size();
@@ -1443,6 +1458,10 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
         out[n] = '\0';
     }
     return WOST_OK;
+}
+
+int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int64_t* length) {
+    return wost_kernel_source_sources(pb, nullptr, 0, out, capacity, length);
 }
 
 int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments) {

@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -16,6 +17,7 @@
 #include <map>
 #include <mutex>
 #include <sstream>
+#include <thread>
 #include <vector>
 
 // Header sources embedded at build time (Makefile: wost_embedded.cpp).
@@ -167,6 +169,83 @@ std::string value_body(const DField& fd, const DTerm* terms, const DFactor* fact
     return o.str();
 }
 
+// Multi-source kernels with Options::param_sources: the source fields' coefficients and
+// factor parameters are read from the program buffer (uniform loads through the constant
+// address space) instead of compiled in as literals, so that the kernel's source -- and its
+// hiprtc compile -- depends on the sources' structure (factor kinds, term counts, monomial
+// exponents, grid shapes) and not on where the electrodes are. The C5 Wenner survey
+// launches every electrode group with other transmitters: with literals its first survey
+// compiles 36 kernels (~22 s of hiprtc one after another, profiles/r06_ab/r06s8), with
+// parameters 2 (4.6 s) -- but its warm survey runs 5% slower on the loads
+// (profiles/r06_ab/r06s9), so literals stay the default and the compiles run concurrently
+// instead (jit_get_kernel). The same float values enter the same operations: the bits of
+// a single-source solve (tests/test_gpu_multisource.py).
+std::string pv(size_t off) {
+    std::ostringstream o;
+    o << "pv(pb, " << off << "u)";
+    return o.str();
+}
+
+std::string factor_call_param(const DFactor& f, size_t foff) {
+    const float* p = f.p;
+    const size_t p0 = foff + offsetof(DFactor, p);
+    auto P = [&](int k) { return pv(p0 + 4 * (size_t)k); };
+    std::ostringstream o;
+    switch (f.kind) {
+    case WOST_FK_MONO:
+        o << "wost::fv_mono(x, y, " << (int)p[0] << ", " << (int)p[1] << ")";
+        break;
+    case WOST_FK_EXP_QUAD: {
+        const bool diag = exp_quad_is_diag(p);   // structure: the interpreter makes the same choice
+        o << (diag ? "wost::fv_exp_quad_diag(x, y" : "wost::fv_exp_quad(x, y");
+        for (int k = 0; k < (diag ? 4 : 8); ++k) o << ", " << P(k);
+        o << ")";
+        break;
+    }
+    case WOST_FK_SIN_LIN:
+    case WOST_FK_COS_LIN:
+    case WOST_FK_SIGMOID_LIN:
+        o << (f.kind == WOST_FK_SIN_LIN ? "wost::fv_sin_lin" : f.kind == WOST_FK_COS_LIN ? "wost::fv_cos_lin"
+                                                                                         : "wost::fv_sigmoid_lin")
+          << "(x, y, " << P(0) << ", " << P(1) << ", " << P(2) << ")";
+        break;
+    case WOST_FK_SIGMOID_RADIAL:
+        o << "wost::fv_sigmoid_radial(x, y, " << P(0) << ", " << P(1) << ", " << P(2) << ", " << P(3) << ")";
+        break;
+    case WOST_FK_IND_BOX:
+        o << "wost::fv_ind_box(x, y, " << P(0) << ", " << P(1) << ", " << P(2) << ", " << P(3) << ")";
+        break;
+    case WOST_FK_IND_DISK:
+        o << "wost::fv_ind_disk(x, y, " << P(0) << ", " << P(1) << ", " << P(2) << ")";
+        break;
+    case WOST_FK_GRID:   // the shape and the offset stay literals (structure)
+        o << "wost::fv_grid(grid + " << (int)p[6] << ", x, y, " << P(0) << ", " << P(1) << ", " << P(2) << ", " << P(3)
+          << ", " << (int)p[4] << ", " << (int)p[5] << ")";
+        break;
+    default:
+        o << "__builtin_nanf(\"\")";
+    }
+    return o.str();
+}
+
+// value_body with the coefficients and factor parameters read from the program buffer
+std::string value_body_param(const DField& fd, const DTerm* terms, const DFactor* factors, int n_terms_total) {
+    std::ostringstream o;
+    const size_t toff = sizeof(DProgram), foff = sizeof(DProgram) + sizeof(DTerm) * (size_t)n_terms_total;
+    o << "        float acc = 0.0f;\n";
+    for (int t = 0; t < fd.n_terms; ++t) {
+        const int ti = fd.first_term + t;
+        const DTerm& tm = terms[ti];
+        o << "        { float t = " << pv(toff + sizeof(DTerm) * (size_t)ti + offsetof(DTerm, coef)) << ";";
+        for (int k = 0; k < tm.nf; ++k)
+            o << " t = t * " << factor_call_param(factors[tm.first + k], foff + sizeof(DFactor) * (size_t)(tm.first + k))
+              << ";";
+        o << " acc = acc + t; }\n";
+    }
+    o << "        return acc;\n";
+    return o.str();
+}
+
 // The saturation predicate of a factor (wost_device.h sat_*), "true" for the
 // indicators (zero derivatives everywhere), "" for a kind without one.
 std::string sat_call(const DFactor& f) {
@@ -276,7 +355,9 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
             if (!cur.empty()) mkdir(cur.c_str(), 0755);
         }
     }
-    std::string tmp = dir + "/" + name + ".tmp." + std::to_string(getpid());
+    // (the thread too: two threads of one process may compile the same kernel at once)
+    std::string tmp = dir + "/" + name + ".tmp." + std::to_string(getpid()) + "." +
+                      std::to_string(std::hash<std::thread::id>{}(std::this_thread::get_id()));
     {
         std::ofstream f(tmp, std::ios::binary);
         if (!f) return;
@@ -417,18 +498,25 @@ std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, cons
     if (opt.tree_batch >= 1) o << "#define WOST_TREE_BATCH " << (opt.tree_batch >= 4 ? 4 : opt.tree_batch >= 2 ? 2 : 1) << "\n";
     o << "// generated by libwost (wost_jit.cpp): walk kernel, mode " << mode << "\n"
       << "#include \"wost_walk.h\"\n\nnamespace {\nstruct GenFields {\n"
-      << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n";
+      << "    const float* grid;   // tabulated field values (WOST_FK_GRID) in the program buffer\n"
+      << "    const char* pb;      // the program buffer (multi-source kernels read the sources' parameters)\n"
+      << "    __device__ __forceinline__ static float pv(const char* p, unsigned off) {\n"
+      << "        return *(const __attribute__((address_space(4))) float*)(p + off);\n    }\n";
     o << "    __device__ __forceinline__ bool has_g() const { return " << (fG.present ? "true" : "false") << "; }\n";
     o << "    __device__ __forceinline__ float g(float x, float y) const {\n"
       << (fG.present ? value_body(fG, terms, factors) : "        return 0.0f;\n") << "    }\n";
+    // (a multi-source kernel never calls f(): its walks score the sources through f_multi)
     o << "    __device__ __forceinline__ float f(float x, float y) const {\n"
-      << (fF.present ? value_body(fF, terms, factors) : "        return 0.0f;\n") << "    }\n";
+      << (fF.present && n_sources == 1 ? value_body(fF, terms, factors) : "        return 0.0f;\n") << "    }\n";
     if (n_sources > 1) {   // multi-source: every source's value, each with f()'s operation sequence
         o << "    __device__ __forceinline__ void f_multi(float x, float y, float* out) const {\n";
         for (int s = 0; s < n_sources; ++s) {
             const DField& fs = hdr.field[s == 0 ? SLOT_F : SLOT_EXTRA + s - 1];
             o << "        out[" << s << "] = [&]() {\n"
-              << (fs.present ? value_body(fs, terms, factors) : "        return 0.0f;\n") << "        }();\n";
+              << (!fs.present          ? std::string("        return 0.0f;\n")
+                  : opt.param_sources ? value_body_param(fs, terms, factors, hdr.n_terms_total)
+                                      : value_body(fs, terms, factors))
+              << "        }();\n";
         }
         o << "    }\n";
     }
@@ -551,7 +639,7 @@ std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, cons
       << "wost_walk_jit(const wost::WalkArgs A) {\n"
       << "    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];\n"
       << "    const GenFields fld{reinterpret_cast<const float*>(A.prog + "
-      << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
+      << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull), A.prog};\n"
       << "    wost::walk_body<" << (neu ? "true" : "false") << ", " << (src ? "true" : "false") << ", "
       << (delta ? "true" : "false") << ", " << (tree ? "true" : "false") << ", " << (record ? "true" : "false")
       << ", " << n_sources << ", " << (mode_fix(mode) ? "true" : "false") << ", "
@@ -560,7 +648,7 @@ std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, cons
         o << "extern \"C\" __global__ void __launch_bounds__(256)\n"
           << "wost_point_alpha_jit(const char* prog, const float2* pts, long long n, float* out) {\n"
           << "    const GenFields fld{reinterpret_cast<const float*>(prog + "
-          << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull)};\n"
+          << program_grid_offset(hdr.n_terms_total, hdr.n_factors_total) << "ull), prog};\n"
           << "    wost::point_alpha_body(pts, (int64_t)n, out, fld);\n}\n";
     return o.str();
 }
@@ -584,12 +672,15 @@ bool jit_get_kernel(const Options& opt, int device, const std::string& source, h
     std::snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)h);
     const std::string key = std::to_string(device) + ":" + arch + ":" + hex;
 
-    std::lock_guard<std::mutex> lock(g_mu);
-    auto it = g_modules.find(key);
-    if (it != g_modules.end()) {
-        *fn = it->second.fn;
-        if (alpha_fn) *alpha_fn = it->second.alpha_fn;
-        return true;
+    {   // the in-memory cache (the lock is not held during a compile: the handles of a survey's
+        // concurrent threads compile their kernels at once -- hiprtc is thread-safe)
+        std::lock_guard<std::mutex> lock(g_mu);
+        auto it = g_modules.find(key);
+        if (it != g_modules.end()) {
+            *fn = it->second.fn;
+            if (alpha_fn) *alpha_fn = it->second.alpha_fn;
+            return true;
+        }
     }
     std::vector<char> code;
     const std::string dir = cache_dir();
@@ -618,7 +709,14 @@ bool jit_get_kernel(const Options& opt, int device, const std::string& source, h
     }
     if (hipModuleGetFunction(&e.alpha_fn, e.mod, "wost_point_alpha_jit") != hipSuccess) e.alpha_fn = nullptr;
     (void)hipGetLastError();   // a source without the alpha kernel leaves a lookup error behind
-    g_modules[key] = e;
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_modules.find(key);
+    if (it != g_modules.end()) {   // another thread loaded the same kernel meanwhile: use its module
+        (void)hipModuleUnload(e.mod);
+        e = it->second;
+    } else {
+        g_modules[key] = e;
+    }
     *fn = e.fn;
     if (alpha_fn) *alpha_fn = e.alpha_fn;
     return true;

@@ -52,6 +52,8 @@ struct Options {
     int fused_scan = 1;
     int refill_min = -1;            // idle lanes that trigger a refill (-1: WOST_REFILL_MIN)
     int philox_ahead = -1;          // Philox words one step ahead (-1: off)
+    int param_sources = 0;          // multi-source kernels read the sources' parameters from the
+                                    // program buffer (one compile per source structure; wost_jit.cpp)
     // work queue (wost_api.hip solve_impl; -1 / 0: the call's own shape)
     int chunk0 = -1;
     int chunk_min = -1;

@@ -102,9 +102,11 @@ def _problem(dxy, nxy, g, f, sigma, alpha, compat, device, sigma_bar):
 
 
 def kernel_source(dirichletBoundary, dirichletBoundaryFunction=None, neumannBoundary=None, source=None,
-                  sigma=None, alpha=None, *, sigma_bar: float | None = None, compat: str = "reference") -> str:
+                  sigma=None, alpha=None, *, sigma_bar: float | None = None, compat: str = "reference",
+                  sources=None) -> str:
     """HIP source of the field-specialised walk kernel a WostSolver_2D with these
-    arguments would compile (no device needed; wost_kernel_source)."""
+    arguments would compile (no device needed; wost_kernel_source). sources: the fields
+    of a multi-source solve (solve_sources; wost_kernel_source_sources)."""
     dxy = np.asarray(_np(dirichletBoundary.points), dtype=np.float32).reshape(-1, 2)
     nxy = None if neumannBoundary is None else np.asarray(_np(neumannBoundary.points), dtype=np.float32).reshape(-1, 2)
     conv = _Converter(_bounds_of(dxy, nxy))
@@ -117,10 +119,14 @@ def kernel_source(dirichletBoundary, dirichletBoundaryFunction=None, neumannBoun
     if compat not in _lib.COMPAT:
         raise ValueError(f"compat must be one of {sorted(_lib.COMPAT)}")
     prob, keep = _problem(dxy, nxy, g, f, s, a, compat, 0, sigma_bar)
+    packed = [_lib.make_field(conv(x, "source")) for x in (sources or [])]
+    arr = (ctypes.POINTER(_lib.WostField) * max(1, len(packed)))(*[ctypes.pointer(wf) for wf, _ in packed])
     n = ctypes.c_int64(0)
-    _lib.check(_lib.lib.wost_kernel_source(ctypes.byref(prob), None, 0, ctypes.byref(n)), "wost_kernel_source")
+    call = lambda buf, cap: _lib.lib.wost_kernel_source_sources(ctypes.byref(prob), arr, len(packed), buf, cap,
+                                                                 ctypes.byref(n))
+    _lib.check(call(None, 0), "wost_kernel_source")
     buf = ctypes.create_string_buffer(n.value + 1)
-    _lib.check(_lib.lib.wost_kernel_source(ctypes.byref(prob), buf, n.value + 1, ctypes.byref(n)), "wost_kernel_source")
+    _lib.check(call(buf, n.value + 1), "wost_kernel_source")
     return buf.value.decode()
 
 

@@ -452,7 +452,7 @@ int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_seg
  * default walk for walk. Names (dcrmontecarlo_amd/csrc/wost_options.h): tree_pool,
  * pool_near, pool_slots, pool_near_waves, pool_min_push, tree_lds, tree_lds_block,
  * tree_share, tree_share_min, tree_share_descent, tree_batch, tree_qmargin, jit_waves,
- * const_vertices, jit_slp, walk_block, fused_scan, refill_min, philox_ahead, chunk0,
+ * const_vertices, jit_slp, walk_block, fused_scan, refill_min, philox_ahead, param_sources, chunk0,
  * chunk_min, chunk_max, adaptive_chunk, grid_blocks_per_cu, lds_pad_bytes.
  * WOST_ERR_INVALID_ARG for an unknown name or a value out of range; WOST_ERR_UNSUPPORTED
  * for a study-build-only name (exp_flags, tree_iter_stats) in the product library. The
@@ -472,6 +472,11 @@ int wost_options_report(const wost_handle* h, char* out, int64_t capacity, int64
  * capacity - 1) is copied to out when out != NULL. Compile it against
  * wost.h, dcrmontecarlo_amd/csrc/wost_device.h and wost_walk.h. */
 int wost_kernel_source(const wost_problem* problem, char* out, int64_t capacity, int64_t* length);
+/* The same for a multi-source solve (wost_set_sources' n_sources fields; 0: the problem's
+ * own source, as wost_kernel_source), with the sources compiled in as literals (the
+ * default; option param_sources = 1 reads them from the program buffer instead). */
+int wost_kernel_source_sources(const wost_problem* problem, const wost_field* const* sources, int32_t n_sources,
+                               char* out, int64_t capacity, int64_t* length);
 
 /* Device evaluation of the handle's fields at points (for tests and for the
  * host API): which = 0 g, 1 f, 2 sigma, 3 alpha (value, d/dx, d/dy, Laplacian

@@ -35,9 +35,13 @@ def _sources(sc, n):
     return out
 
 
+@pytest.mark.parametrize("param", [0, 1])
 @pytest.mark.parametrize("name", ["poisson_square", "dcr_dipole", "variable_coefficients"])
-def test_each_source_equals_its_single_source_solve(gpu_available, name):
+def test_each_source_equals_its_single_source_solve(gpu_available, name, param):
+    """param = 1 (option param_sources): the multi-source kernel reads the sources'
+    parameters from the program buffer instead of literals -- the same bits."""
     sc, s = _solver(name)
+    s.set_option("param_sources", param)
     pts = sc.points[:5]
     W, seed = 3000, 23
     srcs = _sources(sc, 3)
