@@ -228,8 +228,12 @@ std::string factor_call_param(const DFactor& f, size_t foff) {
     return o.str();
 }
 
-// value_body with the coefficients and factor parameters read from the program buffer
-std::string value_body_param(const DField& fd, const DTerm* terms, const DFactor* factors, int n_terms_total) {
+// value_body with the coefficients and factor parameters read from the program buffer.
+// canon[j]: the factor whose parameters factor j reads -- the first one with the same kind
+// and parameters (a Wenner group's transmitters share electrodes: the same Gaussian then
+// reads the same words, and the compiler evaluates it once, as it does with literals).
+std::string value_body_param(const DField& fd, const DTerm* terms, const DFactor* factors, int n_terms_total,
+                             const std::vector<int>& canon) {
     std::ostringstream o;
     const size_t toff = sizeof(DProgram), foff = sizeof(DProgram) + sizeof(DTerm) * (size_t)n_terms_total;
     o << "        float acc = 0.0f;\n";
@@ -238,8 +242,8 @@ std::string value_body_param(const DField& fd, const DTerm* terms, const DFactor
         const DTerm& tm = terms[ti];
         o << "        { float t = " << pv(toff + sizeof(DTerm) * (size_t)ti + offsetof(DTerm, coef)) << ";";
         for (int k = 0; k < tm.nf; ++k)
-            o << " t = t * " << factor_call_param(factors[tm.first + k], foff + sizeof(DFactor) * (size_t)(tm.first + k))
-              << ";";
+            o << " t = t * "
+              << factor_call_param(factors[tm.first + k], foff + sizeof(DFactor) * (size_t)canon[tm.first + k]) << ";";
         o << " acc = acc + t; }\n";
     }
     o << "        return acc;\n";
@@ -510,11 +514,20 @@ std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, cons
       << (fF.present && n_sources == 1 ? value_body(fF, terms, factors) : "        return 0.0f;\n") << "    }\n";
     if (n_sources > 1) {   // multi-source: every source's value, each with f()'s operation sequence
         o << "    __device__ __forceinline__ void f_multi(float x, float y, float* out) const {\n";
+        std::vector<int> canon(hdr.n_factors_total);   // (value_body_param)
+        for (int j = 0; j < hdr.n_factors_total; ++j) {
+            canon[j] = j;
+            for (int i = 0; i < j; ++i)
+                if (factors[i].kind == factors[j].kind && std::memcmp(factors[i].p, factors[j].p, sizeof(factors[j].p)) == 0) {
+                    canon[j] = i;
+                    break;
+                }
+        }
         for (int s = 0; s < n_sources; ++s) {
             const DField& fs = hdr.field[s == 0 ? SLOT_F : SLOT_EXTRA + s - 1];
             o << "        out[" << s << "] = [&]() {\n"
               << (!fs.present          ? std::string("        return 0.0f;\n")
-                  : opt.param_sources ? value_body_param(fs, terms, factors, hdr.n_terms_total)
+                  : opt.param_sources ? value_body_param(fs, terms, factors, hdr.n_terms_total, canon)
                                       : value_body(fs, terms, factors))
               << "        }();\n";
         }
