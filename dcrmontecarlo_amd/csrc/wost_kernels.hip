@@ -203,16 +203,16 @@ constexpr int kReduceBlock = 256;
 
 // The walk launch's statistics (the per-wave records after the control words, wost_walk.h
 // kCtlWords) summed up by one workgroup: lstats[0] earliest wave start, [1] latest dequeue,
-// [2] latest wave end (wall-clock ticks), [4] loop iterations of the wave that ended last
-// and [5] its duration, [6] the most iterations of any wave, [7] waves. A later launch of
-// the same solve combines with the earlier ones' values ([0] the first start, [1]/[2]/[4]/
-// [5] the last launch's, [6] the maximum).
+// [2] latest wave end (wall-clock ticks), [3] the longest walk, [4] loop iterations of the
+// wave that ended last and [5] its duration, [6] the most iterations of any wave, [7] waves.
+// A later launch of the same solve combines with the earlier ones' values ([0] the first
+// start, [1]/[2]/[4]/[5] the last launch's, [3]/[6] the maximum).
 __device__ void reduce_wave_stats(const uint4* __restrict__ ws, int64_t n_waves, unsigned long long* lstats,
                                   int first_batch) {
     __shared__ unsigned long long s_start[kReduceBlock], s_deq[kReduceBlock], s_end[kReduceBlock];
-    __shared__ uint32_t s_it[kReduceBlock], s_dur[kReduceBlock], s_itmax[kReduceBlock];
+    __shared__ uint32_t s_it[kReduceBlock], s_dur[kReduceBlock], s_itmax[kReduceBlock], s_kmax[kReduceBlock];
     unsigned long long st = ~0ull, dq = 0ull, en = 0ull;
-    uint32_t it = 0u, dur = 0u, itmax = 0u;
+    uint32_t it = 0u, dur = 0u, itmax = 0u, kmax = 0u;
     for (int64_t i = threadIdx.x; i < n_waves; i += kReduceBlock) {
         const uint4 a = ws[2 * i], b = ws[2 * i + 1];
         const unsigned long long t0 = (unsigned long long)a.y << 32 | a.x;
@@ -224,9 +224,10 @@ __device__ void reduce_wave_stats(const uint4* __restrict__ ws, int64_t n_waves,
             dur = a.w;
         }
         itmax = b.x > itmax ? b.x : itmax;
+        kmax = b.y > kmax ? b.y : kmax;
     }
     s_start[threadIdx.x] = st; s_deq[threadIdx.x] = dq; s_end[threadIdx.x] = en;
-    s_it[threadIdx.x] = it; s_dur[threadIdx.x] = dur; s_itmax[threadIdx.x] = itmax;
+    s_it[threadIdx.x] = it; s_dur[threadIdx.x] = dur; s_itmax[threadIdx.x] = itmax; s_kmax[threadIdx.x] = kmax;
     __syncthreads();
     for (int h = kReduceBlock / 2; h > 0; h >>= 1) {
         const int t = (int)threadIdx.x;
@@ -239,15 +240,18 @@ __device__ void reduce_wave_stats(const uint4* __restrict__ ws, int64_t n_waves,
                 s_dur[t] = s_dur[t + h];
             }
             s_itmax[t] = s_itmax[t + h] > s_itmax[t] ? s_itmax[t + h] : s_itmax[t];
+            s_kmax[t] = s_kmax[t + h] > s_kmax[t] ? s_kmax[t + h] : s_kmax[t];
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        unsigned long long start = s_start[0], itm = s_itmax[0];
+        unsigned long long start = s_start[0], itm = s_itmax[0], km = s_kmax[0];
         if (!first_batch) {
             start = lstats[0] < start ? lstats[0] : start;
             itm = lstats[6] > itm ? lstats[6] : itm;
+            km = lstats[3] > km ? lstats[3] : km;
         }
+        lstats[3] = km;
         lstats[0] = start;
         lstats[1] = s_deq[0];
         lstats[2] = s_end[0];
@@ -264,8 +268,11 @@ __device__ void reduce_wave_stats(const uint4* __restrict__ ws, int64_t n_waves,
 // the same for every ns, so source k's sums do not depend on the other sources.
 // ctl (may be null): the walk launch's control words (wost_walk.h kCtlWords): workgroup 0
 // resets the queue head for the next launch and, with lstats, sums up the n_waves
-// launch statistics into lstats; every workgroup adds its longest walk to ctl[2]
-// (atomicMax), and the last one to finish moves it to lstats[3] and resets ctl[1..2].
+// launch statistics into lstats (the longest walk among them). Without wave records
+// (n_waves = 0: the segment-tree kernels) every workgroup adds its longest walk to ctl[2]
+// (atomicMax, skipped when not above the value already there), and the last one to finish
+// moves it to lstats[3] and resets ctl[1..2]. (With per-workgroup atomics on every launch
+// C4's 11,760-workgroup reduce took 0.40 ms instead of 0.09: profiles/r06_ab/r06s5.)
 __global__ void __launch_bounds__(kReduceBlock)
 wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ steps,
                   const int64_t* __restrict__ begin, int64_t nblocks, int ns, double* __restrict__ out,
@@ -313,7 +320,7 @@ wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ st
             __syncthreads();
         }
     }
-    if (ctl == nullptr || lstats == nullptr) return;
+    if (ctl == nullptr || lstats == nullptr || n_waves > 0) return;
     // the longest walk: one atomic per workgroup, then the last workgroup to finish moves it
     s_mx[threadIdx.x] = mx_all;
     __syncthreads();
@@ -322,7 +329,8 @@ wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ st
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        atomicMax(ctl + 2, (unsigned long long)s_mx[0]);
+        if ((unsigned long long)s_mx[0] > *(volatile unsigned long long*)(ctl + 2))
+            atomicMax(ctl + 2, (unsigned long long)s_mx[0]);
         __threadfence();
         s_last = atomicAdd(ctl + 1, 1ull) == (unsigned long long)gridDim.x - 1ull;
     }

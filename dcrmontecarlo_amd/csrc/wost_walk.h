@@ -100,9 +100,10 @@ struct WalkArgs {
 };
 
 // The walk launch's control words (WalkArgs::counter): [0] the work-queue head, [1] the
-// block reduce's finished-workgroup count, [2] its longest walk, [3] unused; then per wave
-// two uint4 of launch statistics: {start tick low, high, last dequeue - start, end - start}
-// and {loop iterations, 0, 0, 0} (wave index as in the static chunks). Derived from the
+// block reduce's finished-workgroup count, [2] its longest walk (kernels without wave
+// records), [3] unused; then per wave two uint4 of launch statistics: {start tick low, high,
+// last dequeue - start, end - start} and {loop iterations, longest walk, 0, 0} (wave index
+// as in the static chunks). Derived from the
 // queue's own pointer so that the walk loop keeps no extra pointer live.
 constexpr int kCtlWords = 4;
 WOST_HD constexpr size_t ctl_words(int64_t waves) { return (size_t)kCtlWords + 4 * (size_t)waves; }
@@ -927,6 +928,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
     WOST_KEEP_VGPR(q_iters);
     uint32_t q_taken = 0u;   // walks this wave took from its static chunk and the queue (kAdaptive)
     WOST_KEEP_VGPR(q_taken);
+    uint32_t my_kmax = 0u;   // the longest walk this lane finished (kWaveStats)
     {   // the wave's static first chunk (no atomic at the launch's start, when every wave
         // would hit the one counter at once)
         const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -984,6 +986,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
 #pragma unroll
             for (int s = 0; s < NS; ++s) A.out_val[li * NS + s] = total[s];
             A.out_steps[li] = (uint32_t)k;
+            if (kWaveStats) my_kmax = (uint32_t)k > my_kmax ? (uint32_t)k : my_kmax;
             active = false;
         }
 
@@ -1470,6 +1473,13 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         dD = dd;   // the loop tests the distance of the pre-step point (quirk Q7)
         WOST_PHASE("loop_head");
     }
+    if (kWaveStats) {   // the wave's longest walk (every lane is here)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t other = (uint32_t)__shfl_xor((int)my_kmax, o);
+            my_kmax = other > my_kmax ? other : my_kmax;
+        }
+    }
     if (kWaveStats && lane == 0) {   // the launch statistics (wost_block_reduce sums them up)
         uint4* const wave_stats = reinterpret_cast<uint4*>(A.counter + kCtlWords);
         const uint64_t wv = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -1477,7 +1487,7 @@ __device__ __forceinline__ void walk_body(const WalkArgs& A, const F& fld, unsig
         const uint32_t dur = (uint32_t)end - q_t0;
         const uint64_t start = end - dur;                   // the start's high word, from the end's
         wave_stats[2 * wv] = uint4{(uint32_t)start, (uint32_t)(start >> 32), q_tdeq - q_t0, dur};
-        wave_stats[2 * wv + 1] = uint4{q_iters, 0u, 0u, 0u};
+        wave_stats[2 * wv + 1] = uint4{q_iters, my_kmax, 0u, 0u};
     }
 #if defined(WOST_TREE_ITER_STATS)
     // each lane's counters into the workgroup's study words after its pools (the host
