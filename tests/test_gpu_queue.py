@@ -111,3 +111,29 @@ def test_launch_statistics(gpu_available, name):
     assert t["last_wave_iters"] >= 1 and t["last_wave_ms"] > 0.0
     assert 0.0 <= t["tail_ms"] <= t["span_ms"] <= 1.05 * t["walk_kernel_ms"] + 0.05
     assert t["span_ms"] > 0.0
+
+
+def test_option_api(gpu_available):
+    """wost_set_option / wost_get_option / wost_options_report on a handle: unknown names and
+    out-of-range values raise ValueError, study-build-only names NotImplementedError in the
+    product library; a kernel option rebuilds the handle's kernel and changes no bits."""
+    sc = _scenario("poisson_square")
+    s = sc.solver(device=0)
+    assert s.options_report() == {"build": "product", "non_default": {}}
+    with pytest.raises(ValueError, match="unknown option"):
+        s.set_option("no_such_option", 1)
+    with pytest.raises(ValueError, match="out of range"):
+        s.set_option("pool_slots", 0)
+    with pytest.raises(ValueError):
+        s.set_option("walk_block", 100)          # whole waves only
+    with pytest.raises(NotImplementedError, match="study builds only"):
+        s.set_option("exp_flags", 32)
+    pts = np.ascontiguousarray(sc.points[:4], np.float32)
+    ref = _walks(s, pts, 500, sc, seed=3)
+    s.set_option("walk_block", 512)
+    assert s.get_option("walk_block") == 512.0
+    got = _walks(s, pts, 500, sc, seed=3)
+    assert s.last_timing["block_threads"] == 512
+    assert s.options_report()["non_default"] == {"walk_block": 512}
+    np.testing.assert_array_equal(got[0], ref[0])
+    np.testing.assert_array_equal(got[1], ref[1])
