@@ -1171,8 +1171,9 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         a.chunk = (int)std::max<int64_t>(chunk_min, std::min<int64_t>(chunk_max, share));
         // (a guided queue -- the last ~4 walks per lane in chunks of 64 -- measured no faster
         // on C4 and 10-14% slower on the short-walk scenarios: profiles/r02_ab/guided_queue.log)
-        // (the waves' rate floor assumes the 100 MHz wall clock of gfx950)
-        const bool adaptive = O.adaptive_chunk != 0 && O.chunk_min < 1 && O.chunk_max < 1 && h->tick_khz == 100000.0;
+        // (the waves' rate floor assumes the 100 MHz wall clock of gfx950; the segment-tree
+        // kernels keep their host-sized dequeues)
+        const bool adaptive = !mode_tree(mode) && O.adaptive_chunk != 0 && O.chunk_min < 1 && O.chunk_max < 1 && h->tick_khz == 100000.0;
         a.chunk_share = adaptive ? (uint32_t)std::max<int64_t>(share, a.chunk) : 0u;
         a.waves = (uint32_t)std::min<int64_t>(waves, INT32_MAX);
         if ((int64_t)ctl_words(waves) > h->ctl_cap) {   // more waves than the control block holds

@@ -170,7 +170,7 @@ typedef struct {
     /* the launch's shape -- a function of this call alone (never of an earlier solve):
      * workgroups per CU and their threads, the static first chunk of walks per wave, the
      * host's dequeue size and whether the waves then sized their dequeues from their own
-     * measured walks (wost_set_option "adaptive_chunk") */
+     * measured walks (wost_set_option "adaptive_chunk"; never in the segment-tree kernels) */
     int32_t blocks_per_cu;
     int32_t block_threads;
     int32_t chunk0;
@@ -183,7 +183,7 @@ typedef struct {
      * launch for tail and last wave): first wave start -> last wave end; the last
      * successful dequeue -> last wave end; the wave that ended last: its duration and
      * loop iterations (one walk-step of at least one lane each); the most iterations of
-     * any wave */
+     * any wave (all five 0 for the segment-tree kernels, which keep no wave records) */
     double span_ms;
     double tail_ms;
     double last_wave_ms;

@@ -58,7 +58,7 @@ def test_launch_shape_is_a_function_of_the_call(gpu_available, name, big, small)
         np.testing.assert_array_equal(g[1], ref[1])
         np.testing.assert_array_equal(g[0], ref[0])
     assert ref[1].sum() > 0
-    assert shape["adaptive"] == 1
+    assert shape["adaptive"] == (0 if name == "wenner_topography" else 1)   # tree kernels: host-sized dequeues
 
 
 @pytest.mark.parametrize("name", ["poisson_square", "dcr_dipole", "wenner_topography"])
