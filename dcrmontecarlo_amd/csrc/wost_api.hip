@@ -11,6 +11,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -339,6 +341,34 @@ const std::vector<float>& fixed_screened_table() {
     return t;
 }
 
+// The radial sampler's nodes depend only on the sampler and (screened) sigma_bar: each
+// table is computed once per process (8-14 ms of host time, which every fresh handle's
+// first solve paid; a survey's handles share one sigma_bar). kind 0: Green's, 1: the
+// Jacobian-corrected Green's (compat fixed), 2: screened.
+void sampler_nodes_once(int kind, double sigma_bar, float* out) {
+    static std::mutex mu;
+    static std::map<std::pair<int, uint64_t>, std::vector<float>> cache;
+    uint64_t bits = 0;
+    if (kind == 2) std::memcpy(&bits, &sigma_bar, sizeof(bits));
+    const auto key = std::make_pair(kind, bits);
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) {
+            std::memcpy(out, it->second.data(), sizeof(float) * WOST_SAMPLER_TABLE_N);
+            return;
+        }
+    }
+    std::vector<float> v(WOST_SAMPLER_TABLE_N);
+    if (kind == 2) screened_sampler_nodes(v.data(), WOST_SAMPLER_TABLE_N, sigma_bar);
+    else if (kind == 1) greens_sampler_nodes_jacobian(v.data(), WOST_SAMPLER_TABLE_N);
+    else greens_sampler_nodes(v.data(), WOST_SAMPLER_TABLE_N);
+    std::memcpy(out, v.data(), sizeof(float) * WOST_SAMPLER_TABLE_N);
+    std::lock_guard<std::mutex> lock(mu);
+    if (cache.size() >= 64) cache.clear();
+    cache.emplace(key, std::move(v));
+}
+
 int ensure_table(wost_handle* h) {
     if (h->table_ready) return WOST_OK;
     // sampler nodes, then (delta tracking) the G_norm cells (wost_device.h), then
@@ -347,17 +377,17 @@ int ensure_table(wost_handle* h) {
     const size_t n = table_floats(h->delta, fix_delta);
     h->table.assign(n, 0.f);
     if (fix_delta) {
-        greens_sampler_nodes_jacobian(h->table.data(), WOST_SAMPLER_TABLE_N);   // staged, unused
+        sampler_nodes_once(1, 0.0, h->table.data());   // staged, unused
         greens_norm_cells(h->table.data() + kSamplerFloatsPadded, kGnormCells, (double)kGnormCells / kGnormInvH);
         const std::vector<float>& fx = fixed_screened_table();
         std::memcpy(h->table.data() + kFixTableOffset, fx.data(), sizeof(float) * fx.size());
     } else if (h->delta) {
-        screened_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N, h->sigma_bar);
+        sampler_nodes_once(2, h->sigma_bar, h->table.data());
         greens_norm_cells(h->table.data() + kSamplerFloatsPadded, kGnormCells, (double)kGnormCells / kGnormInvH);
     } else if (h->compat == WOST_COMPAT_FIXED) {
-        greens_sampler_nodes_jacobian(h->table.data(), WOST_SAMPLER_TABLE_N);
+        sampler_nodes_once(1, 0.0, h->table.data());
     } else {
-        greens_sampler_nodes(h->table.data(), WOST_SAMPLER_TABLE_N);
+        sampler_nodes_once(0, 0.0, h->table.data());
     }
     if (!h->d_table) HIP_TRY(hipMalloc(&h->d_table, sizeof(float) * std::max(n, table_floats(true))));
     HIP_TRY(hipMemcpy(h->d_table, h->table.data(), sizeof(float) * n, hipMemcpyHostToDevice));

@@ -143,6 +143,7 @@ void greens_sampler_nodes(float* out, int n) {
         if (i == n - 1) { out[i] = 1.0f; continue; }
         for (int it = 0; it < 200 && hi - lo > 1e-17; ++it) {
             double mid = 0.5 * (lo + hi);
+            if (mid == lo || mid == hi) break;   // adjacent doubles: the bracket no longer moves
             if (cdf(mid) < u) lo = mid; else hi = mid;
         }
         out[i] = (float)(0.5 * (lo + hi));
@@ -158,6 +159,7 @@ void greens_sampler_nodes_jacobian(float* out, int n) {
         double lo = 0.0, hi = 1.0;
         for (int it = 0; it < 200 && hi - lo > 1e-17; ++it) {
             const double mid = 0.5 * (lo + hi);
+            if (mid == lo || mid == hi) break;   // adjacent doubles: the bracket no longer moves
             if (cdf(mid) < u) lo = mid; else hi = mid;
         }
         out[i] = (float)(0.5 * (lo + hi));
