@@ -177,9 +177,10 @@ std::string value_body(const DField& fd, const DTerm* terms, const DFactor* fact
 // launches every electrode group with other transmitters: with literals its first survey
 // compiles 36 kernels (~22 s of hiprtc one after another, profiles/r06_ab/r06s8), with
 // parameters 2 (4.6 s) -- but its warm survey runs 5% slower on the loads
-// (profiles/r06_ab/r06s9), so literals stay the default and the compiles run concurrently
-// instead (jit_get_kernel). The same float values enter the same operations: the bits of
-// a single-source solve (tests/test_gpu_multisource.py).
+// (profiles/r06_ab/r06s9, r06s11), so literals stay the default (the survey's threads
+// request their compiles at once, jit_get_kernel, but ROCm's compiler library runs one
+// in-process compile at a time). The same float values enter the same operations: the bits
+// of a single-source solve (tests/test_gpu_multisource.py).
 std::string pv(size_t off) {
     std::ostringstream o;
     o << "pv(pb, " << off << "u)";
