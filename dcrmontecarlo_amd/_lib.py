@@ -156,6 +156,8 @@ def _load():
         "wost_kernel_source": (c_int32, [POINTER(WostProblem), ctypes.c_char_p, c_int64, POINTER(c_int64)]),
         "wost_kernel_source_sources": (c_int32, [POINTER(WostProblem), POINTER(POINTER(WostField)), c_int32,
                                                  ctypes.c_char_p, c_int64, POINTER(c_int64)]),
+        "wost_jit_compile": (c_int32, [ctypes.c_char_p, ctypes.c_char_p, c_int32, POINTER(c_uint8), c_int64,
+                                       POINTER(c_int64), POINTER(c_int32)]),
         "wost_eval_field": (c_int32, [H, c_int32, POINTER(c_float), c_int64, POINTER(c_float)]),
         "wost_sampler_table": (c_int32, [H, POINTER(c_float), c_int32]),
         "wost_geometry_query": (c_int32, [c_int32, c_int32, POINTER(WostPolyline), POINTER(c_float),

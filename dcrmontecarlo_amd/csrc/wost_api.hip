@@ -1495,6 +1495,25 @@ int wost_kernel_source(const wost_problem* pb, char* out, int64_t capacity, int6
     return wost_kernel_source_sources(pb, nullptr, 0, out, capacity, length);
 }
 
+int wost_jit_compile(const char* source, const char* arch, int32_t in_process, uint8_t* out, int64_t capacity,
+                     int64_t* length, int32_t* used_helper) {
+    if (!source || !arch || !*arch || !length) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    Options opt;   // a new handle's compile options
+    opt.jit_process = in_process ? 0 : 1;
+    std::vector<char> code;
+    std::string err;
+    bool helper = false;
+    if (!jit_compile_host(opt, source, arch, &code, &err, &helper))
+        return fail(WOST_ERR_UNSUPPORTED, "%s", err.c_str());
+    if (used_helper) *used_helper = helper ? 1 : 0;
+    *length = (int64_t)code.size();
+    if (out && capacity < (int64_t)code.size())
+        return fail(WOST_ERR_INVALID_ARG, "capacity %lld < the code object's %lld bytes", (long long)capacity,
+                    (long long)code.size());
+    if (out) std::memcpy(out, code.data(), code.size());
+    return WOST_OK;
+}
+
 int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_segments) {
     if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
     if (leaf_segments < 0 || leaf_segments > 32) return fail(WOST_ERR_INVALID_ARG, "leaf_segments must be in [0, 32]");

@@ -2,11 +2,17 @@
 #include "wost_jit.h"
 #include "wost_internal.h"
 
+#include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hiprtc.h>
+#include <spawn.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
+#include <condition_variable>
 #include <cstddef>
 #include <chrono>
 #include <cmath>
@@ -19,6 +25,10 @@
 #include <sstream>
 #include <thread>
 #include <vector>
+
+#include "wost_rtc.h"
+
+extern char** environ;
 
 // Header sources embedded at build time (Makefile: wost_embedded.cpp).
 extern const char wost_embedded_wost_h[];
@@ -411,43 +421,137 @@ std::string cache_identity(const Options& opt) {
     return id;
 }
 
-bool compile(const Options& opt, const std::string& src, const std::string& arch, std::vector<char>& code,
-             std::string* err) {
-    const char* hdrs[] = {wost_embedded_wost_h, wost_embedded_wost_device_h, wost_embedded_wost_walk_h};
-    const char* names[] = {"wost.h", "wost_device.h", "wost_walk.h"};
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "wost_walk_jit.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
-        *err = "hiprtcCreateProgram failed";
-        return false;
-    }
-    std::string arch_opt = "--offload-arch=" + arch;
-    std::vector<const char*> opts = {arch_opt.c_str()};
+std::vector<std::string> compile_options(const Options& opt, const std::string& arch) {
+    std::vector<std::string> opts = {"--offload-arch=" + arch};
     for (const char* o : kCompileOptions) opts.push_back(o);
     if (slp_off(opt)) opts.push_back("-fno-slp-vectorize");
     const std::string sched = sched_option(opt);
     if (!sched.empty()) {
         opts.push_back("-mllvm");
-        opts.push_back(sched.c_str());
+        opts.push_back(sched);
     }
-    hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
-    if (rc != HIPRTC_SUCCESS) {
-        size_t n = 0;
-        hiprtcGetProgramLogSize(prog, &n);
-        std::string log(n + 1, '\0');
-        if (n) hiprtcGetProgramLog(prog, &log[0]);
-        *err = std::string("hiprtc: ") + hiprtcGetErrorString(rc) + ": " + log.c_str();
-        hiprtcDestroyProgram(&prog);
+    return opts;
+}
+
+// The compile helper next to this library (dcrmontecarlo_amd/wost_jitc), or "" when it is
+// not there (then every compile runs in this process).
+const std::string& helper_path() {
+    static const std::string path = [] {
+        Dl_info info;
+        if (!dladdr(reinterpret_cast<void*>(&helper_path), &info) || !info.dli_fname) return std::string();
+        std::string lib = info.dli_fname;
+        const size_t slash = lib.rfind('/');
+        std::string p = (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/wost_jitc";
+        return access(p.c_str(), X_OK) == 0 ? p : std::string();
+    }();
+    return path;
+}
+
+// At most this many helpers run at once (a survey's handle threads: 2-8): the compiles
+// are CPU work, and the GPU box's share of the host is 16 cores.
+constexpr int kMaxHelpers = 8;
+std::mutex g_helper_mu;
+std::condition_variable g_helper_cv;
+int g_helpers = 0;
+
+// One compile in a child process (wost_jitc): source, code object and the compiler's
+// log pass through files of a private scratch directory. false (and *err) when the helper
+// could not be started or did not produce a code object; the caller then compiles here.
+bool compile_in_helper(const std::string& helper, const std::vector<std::string>& opts, const std::string& src,
+                       std::vector<char>& code, std::string* err) {
+    {
+        std::unique_lock<std::mutex> lock(g_helper_mu);
+        g_helper_cv.wait(lock, [] { return g_helpers < kMaxHelpers; });
+        ++g_helpers;
+    }
+    struct Slot {
+        ~Slot() {
+            { std::lock_guard<std::mutex> lock(g_helper_mu); --g_helpers; }
+            g_helper_cv.notify_one();
+        }
+    } slot;
+    const char* tmp = std::getenv("TMPDIR");
+    std::string dir = std::string(tmp && *tmp ? tmp : "/tmp") + "/wost_jitc.XXXXXX";
+    if (!mkdtemp(&dir[0])) {
+        *err = std::string("mkdtemp: ") + std::strerror(errno);
         return false;
     }
-    size_t n = 0;
-    hiprtcGetCodeSize(prog, &n);
-    code.resize(n);
-    hiprtcGetCode(prog, code.data());
-    hiprtcDestroyProgram(&prog);
-    return true;
+    const std::string src_path = dir + "/kernel.hip", out_path = dir + "/kernel.hsaco", log_path = dir + "/log.txt";
+    struct Cleanup {
+        const std::string &d, &a, &b, &c;
+        ~Cleanup() {
+            unlink(a.c_str());
+            unlink(b.c_str());
+            unlink(c.c_str());
+            rmdir(d.c_str());
+        }
+    } cleanup{dir, src_path, out_path, log_path};
+    {
+        std::ofstream f(src_path, std::ios::binary);
+        f.write(src.data(), (std::streamsize)src.size());
+        if (!f) {
+            *err = "cannot write " + src_path;
+            return false;
+        }
+    }
+    std::vector<std::string> args = {helper, src_path, out_path};
+    args.insert(args.end(), opts.begin(), opts.end());
+    std::vector<char*> argv;
+    for (std::string& a : args) argv.push_back(&a[0]);
+    argv.push_back(nullptr);
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+    posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);
+    posix_spawn_file_actions_addopen(&fa, 2, log_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+    pid_t pid = -1;
+    const int rc = posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv.data(), environ);
+    posix_spawn_file_actions_destroy(&fa);
+    if (rc != 0) {
+        *err = std::string("posix_spawn(") + helper + "): " + std::strerror(rc);
+        return false;
+    }
+    int status = 0;
+    while (waitpid(pid, &status, 0) < 0) {
+        if (errno != EINTR) {
+            *err = std::string("waitpid: ") + std::strerror(errno);
+            return false;
+        }
+    }
+    if (WIFEXITED(status) && WEXITSTATUS(status) == 0 && read_file(out_path, code)) return true;
+    std::vector<char> log;
+    read_file(log_path, log);
+    *err = "wost_jitc " + (WIFEXITED(status) ? "exit status " + std::to_string(WEXITSTATUS(status))
+                                             : "signal " + std::to_string(WTERMSIG(status))) +
+           ": " + std::string(log.begin(), log.end());
+    return false;
+}
+
+// A compile for `arch`, in the helper when there is one and opt.jit_process is set
+// (the same code object either way), else -- or when the helper failed -- in this process.
+bool compile(const Options& opt, const std::string& src, const std::string& arch, std::vector<char>& code,
+             std::string* err, bool* in_helper = nullptr) {
+    const std::vector<std::string> opts = compile_options(opt, arch);
+    if (in_helper) *in_helper = false;
+    if (opt.jit_process && !helper_path().empty()) {
+        std::string herr;
+        if (compile_in_helper(helper_path(), opts, src, code, &herr)) {
+            if (in_helper) *in_helper = true;
+            return true;
+        }
+        std::fprintf(stderr, "libwost: compile helper failed, compiling in this process: %s\n", herr.c_str());
+    }
+    return rtc_compile(src, opts, &code, err);
 }
 
 }  // namespace
+
+bool jit_compile_host(const Options& opt, const std::string& source, const std::string& arch,
+                      std::vector<char>* code, std::string* err, bool* in_helper) {
+    return compile(opt, source, arch, *code, err, in_helper);
+}
+
+bool jit_helper_available() { return !helper_path().empty(); }
 
 bool jit_const_dirichlet(const Options& o, int nd) { return nd <= o.const_vertices; }
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <vector>
 
 #include "wost_device.h"
 #include "wost_options.h"
@@ -54,5 +55,13 @@ std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, cons
 // *compile_ms: host time of the hiprtc compile (0 when a cache had the code).
 bool jit_get_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn, std::string* err,
                     hipFunction_t* alpha_fn = nullptr, double* compile_ms = nullptr);
+
+// A compile of `source` for `arch` with the options `opt` selects, without a device (the
+// helper process wost_jitc when there is one and opt.jit_process is set, else in this
+// process; *in_helper says which ran). For wost_jit_compile and the tests.
+bool jit_compile_host(const Options& opt, const std::string& source, const std::string& arch,
+                      std::vector<char>* code, std::string* err, bool* in_helper);
+// Whether the compile helper is installed next to this library.
+bool jit_helper_available();
 
 }  // namespace wost

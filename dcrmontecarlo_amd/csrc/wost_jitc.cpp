@@ -1,0 +1,44 @@
+// wost_jitc -- libwost's compile helper: one field-specialised walk kernel per run.
+//
+//   wost_jitc <source file> <code object file> <hiprtc option>...
+//
+// Reads the generated source, compiles it with hiprtc and the given options against the
+// headers embedded in this binary (the same bytes as libwost's), writes the code object,
+// and exits 0; on a compile error it prints the compiler's log on stderr and exits 1.
+// It never touches a GPU: libwost (wost_jit.cpp) starts one per compile so that the
+// compiles of concurrent handles overlap, and loads the code object itself.
+#include <cstdio>
+#include <fstream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+#include "wost_rtc.h"
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        std::fprintf(stderr, "usage: %s <source file> <code object file> <hiprtc option>...\n", argv[0]);
+        return 2;
+    }
+    std::ifstream in(argv[1], std::ios::binary);
+    if (!in) {
+        std::fprintf(stderr, "wost_jitc: cannot read %s\n", argv[1]);
+        return 2;
+    }
+    const std::string source((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    std::vector<std::string> options(argv + 3, argv + argc);
+    std::vector<char> code;
+    std::string log;
+    if (!wost::rtc_compile(source, options, &code, &log)) {
+        std::fprintf(stderr, "%s\n", log.c_str());
+        return 1;
+    }
+    std::ofstream out(argv[2], std::ios::binary);
+    out.write(code.data(), (std::streamsize)code.size());
+    out.close();
+    if (!out) {
+        std::fprintf(stderr, "wost_jitc: cannot write %s\n", argv[2]);
+        return 2;
+    }
+    return 0;
+}

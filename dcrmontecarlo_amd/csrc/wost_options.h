@@ -54,6 +54,8 @@ struct Options {
     int philox_ahead = -1;          // Philox words one step ahead (-1: off)
     int param_sources = 0;          // multi-source kernels read the sources' parameters from the
                                     // program buffer (one compile per source structure; wost_jit.cpp)
+    int jit_process = 1;            // compile in the helper process wost_jitc (the same code object;
+                                    // concurrent handles' compiles overlap), 0: in this process
     // work queue (wost_api.hip solve_impl; -1 / 0: the call's own shape)
     int chunk0 = -1;
     int chunk_min = -1;

@@ -452,7 +452,7 @@ int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_seg
  * default walk for walk. Names (dcrmontecarlo_amd/csrc/wost_options.h): tree_pool,
  * pool_near, pool_slots, pool_near_waves, pool_min_push, tree_lds, tree_lds_block,
  * tree_share, tree_share_min, tree_share_descent, tree_batch, tree_qmargin, jit_waves,
- * const_vertices, jit_slp, walk_block, fused_scan, refill_min, philox_ahead, param_sources, chunk0,
+ * const_vertices, jit_slp, walk_block, fused_scan, refill_min, philox_ahead, param_sources, jit_process, chunk0,
  * chunk_min, chunk_max, adaptive_chunk, grid_blocks_per_cu, lds_pad_bytes.
  * WOST_ERR_INVALID_ARG for an unknown name or a value out of range; WOST_ERR_UNSUPPORTED
  * for a study-build-only name (exp_flags, tree_iter_stats) in the product library. The
@@ -477,6 +477,18 @@ int wost_kernel_source(const wost_problem* problem, char* out, int64_t capacity,
  * default; option param_sources = 1 reads them from the program buffer instead). */
 int wost_kernel_source_sources(const wost_problem* problem, const wost_field* const* sources, int32_t n_sources,
                                char* out, int64_t capacity, int64_t* length);
+
+/* Compiles a generated walk-kernel source (wost_kernel_source) for the gfx target `arch`
+ * ("gfx950") with the compile options of a new handle, without a device: in the compile
+ * helper wost_jitc (installed next to libwost.so) unless in_process, else -- or when the
+ * helper is missing or fails -- in this process; *used_helper (optional) says which ran.
+ * Handles compile their kernels the same way (option jit_process, default 1): ROCm's
+ * compiler library serialises one process's compiles, so concurrent handles (a survey's
+ * threads) overlap theirs only in helpers. *length = the code object's size; it is copied
+ * to out when out != NULL (WOST_ERR_INVALID_ARG when capacity is smaller). No reference
+ * counterpart (the reference's TorchScript kernels compile in the interpreter). */
+int wost_jit_compile(const char* source, const char* arch, int32_t in_process, uint8_t* out, int64_t capacity,
+                     int64_t* length, int32_t* used_helper);
 
 /* Device evaluation of the handle's fields at points (for tests and for the
  * host API): which = 0 g, 1 f, 2 sigma, 3 alpha (value, d/dx, d/dy, Laplacian
