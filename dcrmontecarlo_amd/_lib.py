@@ -114,6 +114,7 @@ def _load():
                                  POINTER(c_uint32)]),
         "wost_solve_history": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int32, c_float, c_uint64,
                                          POINTER(c_double), POINTER(c_float), POINTER(c_uint32), POINTER(c_float)]),
+        "wost_prepare_sources": (c_int32, [H, POINTER(POINTER(WostField)), c_int32, c_int64]),
         "wost_set_sources": (c_int32, [H, POINTER(POINTER(WostField)), c_int32]),
         "wost_solve_multi": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
                                        c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_float),

@@ -285,6 +285,23 @@ bool exact_trig_of(const wost_handle* h) {
     return (int)(h->nverts.size() / 2) - 1 >= 3;
 }
 
+// The source of the field-specialised kernel for `mode` with the program `prog` (the
+// handle's own, or wost_prepare_multi's with other sources): the handle's polylines,
+// options and trig choice, the launch's workgroup, staging and polyline placement.
+int jit_source(const wost_handle* h, const Program& prog, int mode, bool record, int ns, int block,
+               bool global_polylines, int tree_stage, std::string* src) {
+    const int nn = (int)(h->nverts.size() / 2);
+    std::vector<float> phi;   // a compiled-in Neumann polyline carries the device's segment angles
+    if (jit_const_neumann(h->opt, mode, nn) && nn >= 2) {
+        phi.resize(nn - 1);
+        HIP_TRY(hipMemcpy(phi.data(), h->d_seg_phi, sizeof(float) * phi.size(), hipMemcpyDeviceToHost));
+    }
+    *src = jit_generate(h->opt, mode, *prog.hdr(), prog.terms(), prog.factors(), h->dverts.data(),
+                        (int)(h->dverts.size() / 2), h->nverts.data(), nn, record, ns, block,
+                        phi.empty() ? nullptr : phi.data(), global_polylines, tree_stage, exact_trig_of(h));
+    return WOST_OK;
+}
+
 hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock,
                          bool global_polylines = false, int tree_stage = 0, double* compile_ms = nullptr) {
     if (!h->jit_enabled) return nullptr;
@@ -298,17 +315,8 @@ hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int 
     h->jit_alpha_fn = nullptr;
     h->jit_mode = key;
     h->jit_version = h->prog_version;
-    const int nn = (int)(h->nverts.size() / 2);
-    std::vector<float> phi;   // a compiled-in Neumann polyline carries the device's segment angles
-    if (jit_const_neumann(h->opt, mode, nn) && nn >= 2) {
-        phi.resize(nn - 1);
-        if (hipMemcpy(phi.data(), h->d_seg_phi, sizeof(float) * phi.size(), hipMemcpyDeviceToHost) != hipSuccess)
-            return nullptr;
-    }
-    const std::string src = jit_generate(h->opt, mode, *h->prog.hdr(), h->prog.terms(), h->prog.factors(),
-                                         h->dverts.data(), (int)(h->dverts.size() / 2), h->nverts.data(), nn, record,
-                                         ns, block, phi.empty() ? nullptr : phi.data(), global_polylines, tree_stage,
-                                         exact);
+    std::string src;
+    if (jit_source(h, h->prog, mode, record, ns, block, global_polylines, tree_stage, &src) != WOST_OK) return nullptr;
     std::string err;
     hipFunction_t fn = nullptr;
     hipFunction_t afn = nullptr;
@@ -473,9 +481,8 @@ bool use_tree(const wost_handle* h) {
     return nseg >= 1 && h->tree_min_segments >= 0 && nseg >= h->tree_min_segments;
 }
 
-int walk_mode(const wost_handle* h) {
+int walk_mode_src(const wost_handle* h, bool src) {
     const bool neu = !h->nverts.empty();
-    const bool src = h->fields[SLOT_F].present;
     const bool tree = neu && use_tree(h);
     if (h->compat == WOST_COMPAT_FIXED) {   // the nearest-crossing ray queries (scan or tree)
         if (h->delta) return neu ? (tree ? MODE_FIX_MIXED_DELTA_TREE : MODE_FIX_MIXED_DELTA) : MODE_FIX_DELTA;
@@ -487,6 +494,8 @@ int walk_mode(const wost_handle* h) {
     if (neu) return src ? (tree ? MODE_MIXED_POISSON_TREE : MODE_MIXED_POISSON) : (tree ? MODE_MIXED_TREE : MODE_MIXED);
     return src ? MODE_POISSON : MODE_DIRICHLET;
 }
+
+int walk_mode(const wost_handle* h) { return walk_mode_src(h, h->fields[SLOT_F].present); }
 
 int ensure_tree(wost_handle* h) {
     if (h->tree_ready) return WOST_OK;
@@ -827,6 +836,44 @@ constexpr int64_t kMaxRecordBatchBytes = int64_t(1) << 30;   // device buffer of
 // Walk-range mode (wost_solve_range): walk_begin/walk_end != 0/W solves walks
 // [walk_begin, walk_end) of every point; blocks are then (point, block of the
 // range), point-major, and block_begin/block_end are ignored.
+// The kernel a solve of n_points launches first (its occupancy fallback may then stage
+// less): the workgroup, the segment tree's staging, and whether the polylines are read
+// from global memory. Shared by solve_impl and wost_prepare_multi, so that a prepared
+// kernel is the one the solve looks up.
+struct KernelShape {
+    int block = kWalkBlock, tree_verts = 0, tree_level = kTreeLdsDefaultLevel, tree_lds = 0;
+    bool gpoly = false;
+};
+
+int first_kernel_shape(const wost_handle* h, int mode, int64_t n_points, KernelShape* ks) {
+    *ks = KernelShape{};
+    ks->tree_lds = h->jit_enabled ? tree_lds_records(h, mode, ks->tree_level, &ks->block, &ks->tree_verts) : 0;
+    // option walk_block: the workgroup of the field-specialised scan kernels (a multiple of
+    // 64 up to 1024): larger workgroups share one LDS copy of the sampler and G_norm tables,
+    // so more waves fit a CU than 256-thread workgroups allow (results are the same bits)
+    if (h->jit_enabled && !mode_tree(mode) && h->opt.walk_block > 0) ks->block = h->opt.walk_block;
+    const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
+    const Options& O = h->opt;
+    // polylines whose LDS copy would cost the walk kernel its occupancy are read from
+    // global memory instead (field-specialised kernels; the precompiled ones stage them)
+    // (the staged tree records have their own budget, kTreeLdsMaxBytes)
+    ks->gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0,
+                                                 jit_const_dirichlet(O, nd_)) > kGlobalPolylineLdsBytes;
+    // the brute-force scan of a long Neumann polyline (neumann_scan_both) reads every vertex
+    // at every step: staged in LDS with one 1024-thread workgroup per CU when it fits (a
+    // broadcast LDS read per vertex), else from global memory
+    if (ks->gpoly && h->jit_enabled && jit_fused_neumann_scan(O, mode, nn_)) {
+        int cap = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device));
+        if (walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0, jit_const_dirichlet(O, nd_), false, false,
+                           kTreeStageVertsBlock) <= (size_t)cap) {
+            ks->gpoly = false;
+            ks->block = kTreeStageVertsBlock;
+        }
+    }
+    return WOST_OK;
+}
+
 int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W, int64_t block_begin,
                int64_t block_end, int32_t max_steps, float eps, uint64_t seed, double* block_stats,
                double* point_stats, float* walk_values, uint32_t* walk_steps, float* records, bool multi = false,
@@ -949,33 +996,13 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     } rec_free{d_rec};
     if (records) HIP_TRY(hipMalloc(&d_rec, (size_t)std::min<int64_t>(walks_total, batch_limit) * rec_walk_bytes));
 
-    int block = kWalkBlock, tree_verts = 0;
-    int tree_level = kTreeLdsDefaultLevel;
-    int tree_lds = h->jit_enabled ? tree_lds_records(h, mode, tree_level, &block, &tree_verts) : 0;
-    // option walk_block: the workgroup of the field-specialised scan kernels (a multiple of
-    // 64 up to 1024): larger workgroups share one LDS copy of the sampler and G_norm tables,
-    // so more waves fit a CU than 256-thread workgroups allow (results are the same bits)
-    if (h->jit_enabled && !mode_tree(mode) && h->opt.walk_block > 0) block = h->opt.walk_block;
+    KernelShape ks;
+    if ((rc = first_kernel_shape(h, mode, n_points, &ks)) != WOST_OK) return rc;
+    int block = ks.block, tree_verts = ks.tree_verts, tree_level = ks.tree_level, tree_lds = ks.tree_lds;
+    bool gpoly = ks.gpoly;
     const int nd_ = (int)(h->dverts.size() / 2), nn_ = (int)(h->nverts.size() / 2);
     const Options& O = h->opt;
     double jit_ms = 0.0;
-    // polylines whose LDS copy would cost the walk kernel its occupancy are read from
-    // global memory instead (field-specialised kernels; the precompiled ones stage them)
-    // (the staged tree records have their own budget, kTreeLdsMaxBytes)
-    bool gpoly = h->jit_enabled && walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0,
-                                                  jit_const_dirichlet(O, nd_)) > kGlobalPolylineLdsBytes;
-    // the brute-force scan of a long Neumann polyline (neumann_scan_both) reads every vertex
-    // at every step: staged in LDS with one 1024-thread workgroup per CU when it fits (a
-    // broadcast LDS read per vertex), else from global memory
-    if (gpoly && h->jit_enabled && jit_fused_neumann_scan(O, mode, nn_)) {
-        int cap = 0;
-        HIP_TRY(hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, h->device));
-        if (walk_lds_bytes(mode, nd_, nn_, (int)n_points, 0, jit_const_dirichlet(O, nd_), false, false,
-                           kTreeStageVertsBlock) <= (size_t)cap) {
-            gpoly = false;
-            block = kTreeStageVertsBlock;
-        }
-    }
     auto stage_of = [](int recs, int verts) { return recs > 0 ? (verts > 0 ? 2 : 1) : 0; };
     hipFunction_t jfn = jit_kernel(h, mode, records != nullptr, ns, block, gpoly, stage_of(tree_lds, tree_verts),
                                    &jit_ms);
@@ -1310,6 +1337,32 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     return WOST_OK;
 }
 
+// The handle's fields with sources[0..n) in the source slots (wost_set_sources' conversion).
+int fields_with_sources(const wost_handle* h, const wost_field* const* sources, int32_t n, HostField* out) {
+    if (n < 1 || n > WOST_MAX_SOURCES || !sources)
+        return fail(WOST_ERR_INVALID_ARG, "need 1..%d sources (got %d)", WOST_MAX_SOURCES, n);
+    std::vector<HostField> conv(n);
+    int64_t grid = 0;
+    for (int s = 0; s < n; ++s) {
+        if (!sources[s]) return fail(WOST_ERR_INVALID_ARG, "source %d is NULL", s);
+        char name[32];
+        std::snprintf(name, sizeof(name), "source[%d]", s);
+        int rc = convert_field(sources[s], conv[s], name);
+        if (rc != WOST_OK) return rc;
+        grid += (int64_t)conv[s].grid.size();
+    }
+    for (int s = 0; s < N_SLOTS; ++s)
+        if (s != SLOT_F) grid += (int64_t)h->fields[s].grid.size();
+    if (grid >= (int64_t(1) << 24))
+        return fail(WOST_ERR_INVALID_ARG, "tabulated fields hold %lld values together (limit 2^24)", (long long)grid);
+    for (int s = 0; s < N_FIELDS; ++s) out[s] = h->fields[s];
+    out[SLOT_F] = conv[0];
+    for (int s = 1; s < WOST_MAX_SOURCES; ++s) out[SLOT_EXTRA + s - 1] = s < n ? conv[s] : HostField();
+    return WOST_OK;
+}
+
+std::mutex g_prepare_mu;   // wost_prepare_sources: one segment-tree build per handle
+
 }  // namespace
 
 extern "C" {
@@ -1412,30 +1465,42 @@ int wost_solve_multi(wost_handle* h, const float* points, int64_t n_points, int6
 
 int wost_set_sources(wost_handle* h, const wost_field* const* sources, int32_t n) {
     if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
-    if (n < 1 || n > WOST_MAX_SOURCES || !sources)
-        return fail(WOST_ERR_INVALID_ARG, "need 1..%d sources (got %d)", WOST_MAX_SOURCES, n);
-    std::vector<HostField> conv(n);
-    int64_t grid = 0;
-    for (int s = 0; s < n; ++s) {
-        if (!sources[s]) return fail(WOST_ERR_INVALID_ARG, "source %d is NULL", s);
-        char name[32];
-        std::snprintf(name, sizeof(name), "source[%d]", s);
-        int rc = convert_field(sources[s], conv[s], name);
-        if (rc != WOST_OK) return rc;
-        grid += (int64_t)conv[s].grid.size();
-    }
-    for (int s = 0; s < N_SLOTS; ++s)
-        if (s != SLOT_F) grid += (int64_t)h->fields[s].grid.size();
-    if (grid >= (int64_t(1) << 24))
-        return fail(WOST_ERR_INVALID_ARG, "tabulated fields hold %lld values together (limit 2^24)", (long long)grid);
-    h->fields[SLOT_F] = conv[0];
-    for (int s = 1; s < WOST_MAX_SOURCES; ++s) h->fields[SLOT_EXTRA + s - 1] = s < n ? conv[s] : HostField();
+    std::vector<HostField> f(N_FIELDS);
+    int rc = fields_with_sources(h, sources, n, f.data());
+    if (rc != WOST_OK) return rc;
+    for (int s = 0; s < N_FIELDS; ++s) h->fields[s] = std::move(f[s]);
     h->n_sources = n;
     h->prog_dirty = true;
     HIP_TRY(hipSetDevice(h->device));
     return upload_program(h);
 }
 
+int wost_prepare_sources(wost_handle* h, const wost_field* const* sources, int32_t n, int64_t n_points) {
+    if (!h) return fail(WOST_ERR_INVALID_ARG, "NULL handle");
+    if (n_points < 1) return fail(WOST_ERR_INVALID_ARG, "n_points must be >= 1 (got %lld)", (long long)n_points);
+    std::vector<HostField> f(N_FIELDS);
+    int rc = fields_with_sources(h, sources, n, f.data());
+    if (rc != WOST_OK) return rc;
+    if (!h->jit_enabled)
+        return fail(WOST_ERR_UNSUPPORTED, "multi-source solves need the field-specialised kernel (disabled by wost_set_jit)");
+    Program prog;
+    build_program(f.data(), h->sigma_bar, prog);
+    const int mode = walk_mode_src(h, f[SLOT_F].present);
+    HIP_TRY(hipSetDevice(h->device));
+    if (mode_tree(mode)) {   // the staging choice depends on the tree's size
+        std::lock_guard<std::mutex> lock(g_prepare_mu);
+        if ((rc = ensure_tree(h)) != WOST_OK) return rc;
+    }
+    KernelShape ks;
+    if ((rc = first_kernel_shape(h, mode, n_points, &ks)) != WOST_OK) return rc;
+    const int stage = ks.tree_lds > 0 ? (ks.tree_verts > 0 ? 2 : 1) : 0;
+    std::string src, err;
+    if ((rc = jit_source(h, prog, mode, false, n, ks.block, ks.gpoly, stage, &src)) != WOST_OK) return rc;
+    hipFunction_t fn = nullptr;
+    if (!jit_get_kernel(h->opt, h->device, src, &fn, &err, nullptr, nullptr))
+        return fail(WOST_ERR_UNSUPPORTED, "field-specialised kernel unavailable: %s", err.c_str());
+    return WOST_OK;
+}
 
 int wost_kernel_source_sources(const wost_problem* pb, const wost_field* const* sources, int32_t n_sources,
                                char* out, int64_t capacity, int64_t* length) {

@@ -410,17 +410,6 @@ std::string sched_option(const Options& opt) {
 // spills. Options::jit_slp = 1 keeps the vectoriser (A/B).
 bool slp_off(const Options& opt) { return opt.jit_slp == 0; }
 
-std::string cache_identity(const Options& opt) {
-    std::string id = "fmt" + std::to_string(kCacheFormat);
-    for (const char* o : kCompileOptions) id += std::string("|") + o;
-    if (!sched_option(opt).empty()) id += "|-mllvm " + sched_option(opt);
-    if (slp_off(opt)) id += "|-fno-slp-vectorize";
-    int maj = 0, min = 0, rt = 0;
-    if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) id += "|hiprtc" + std::to_string(maj) + "." + std::to_string(min);
-    if (hipRuntimeGetVersion(&rt) == hipSuccess) id += "|hip" + std::to_string(rt);
-    return id;
-}
-
 std::vector<std::string> compile_options(const Options& opt, const std::string& arch) {
     std::vector<std::string> opts = {"--offload-arch=" + arch};
     for (const char* o : kCompileOptions) opts.push_back(o);
@@ -431,6 +420,59 @@ std::vector<std::string> compile_options(const Options& opt, const std::string& 
         opts.push_back(sched);
     }
     return opts;
+}
+
+// A private scratch directory for one helper run, removed with its files.
+struct Scratch {
+    std::string dir;
+    std::vector<std::string> files;
+    bool ok = false;
+    Scratch() {
+        const char* tmp = std::getenv("TMPDIR");
+        dir = std::string(tmp && *tmp ? tmp : "/tmp") + "/wost_jitc.XXXXXX";
+        ok = mkdtemp(&dir[0]) != nullptr;
+    }
+    std::string file(const char* name) {
+        files.push_back(dir + "/" + name);
+        return files.back();
+    }
+    ~Scratch() {
+        for (const std::string& f : files) unlink(f.c_str());
+        if (ok) rmdir(dir.c_str());
+    }
+};
+
+// Runs `args` (args[0] the program) as a child process with stdin from /dev/null and
+// stdout / stderr into the given files, and waits for it. true when it exited 0; else
+// false and *err says how it ended.
+bool run_child(std::vector<std::string> args, const std::string& out_path, const std::string& err_path,
+               std::string* err) {
+    std::vector<char*> argv;
+    for (std::string& a : args) argv.push_back(&a[0]);
+    argv.push_back(nullptr);
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+    posix_spawn_file_actions_addopen(&fa, 1, out_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+    posix_spawn_file_actions_addopen(&fa, 2, err_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+    pid_t pid = -1;
+    const int rc = posix_spawn(&pid, args[0].c_str(), &fa, nullptr, argv.data(), environ);
+    posix_spawn_file_actions_destroy(&fa);
+    if (rc != 0) {
+        *err = "posix_spawn(" + args[0] + "): " + std::strerror(rc);
+        return false;
+    }
+    int status = 0;
+    while (waitpid(pid, &status, 0) < 0) {
+        if (errno != EINTR) {
+            *err = std::string("waitpid: ") + std::strerror(errno);
+            return false;
+        }
+    }
+    if (WIFEXITED(status) && WEXITSTATUS(status) == 0) return true;
+    *err = WIFEXITED(status) ? "exit status " + std::to_string(WEXITSTATUS(status))
+                             : "signal " + std::to_string(WTERMSIG(status));
+    return false;
 }
 
 // The compile helper next to this library (dcrmontecarlo_amd/wost_jitc), or "" when it is
@@ -447,9 +489,49 @@ const std::string& helper_path() {
     return path;
 }
 
-// At most this many helpers run at once (a survey's handle threads: 2-8): the compiles
-// are CPU work, and the GPU box's share of the host is 16 cores.
-constexpr int kMaxHelpers = 8;
+// The hiprtc library the helper compiles with (wost_jitc --identity, run once per
+// process), or "" when there is no helper or it cannot run: compiles stay in this process.
+const std::string& helper_identity() {
+    static const std::string id = [] {
+        if (helper_path().empty()) return std::string();
+        Scratch sc;
+        if (!sc.ok) return std::string();
+        const std::string out = sc.file("identity.txt"), log = sc.file("log.txt");
+        std::string err;
+        std::vector<char> text;
+        if (!run_child({helper_path(), "--identity"}, out, log, &err) || !read_file(out, text)) {
+            std::fprintf(stderr, "libwost: compile helper %s unusable (%s); compiling in this process\n",
+                         helper_path().c_str(), err.c_str());
+            return std::string();
+        }
+        std::string s(text.begin(), text.end());
+        while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
+        return s;
+    }();
+    return id;
+}
+
+bool use_helper(const Options& opt) { return opt.jit_process != 0 && !helper_identity().empty(); }
+
+// The cache key's compile identity: the format, the compile options, the compiler -- the
+// hiprtc library that compiles (the helper's, or the one this process bound: a process that
+// imported PyTorch-ROCm first binds PyTorch's own copy, another ROCm release's compiler) --
+// and the HIP runtime that loads the code.
+std::string cache_identity(const Options& opt) {
+    std::string id = "fmt" + std::to_string(kCacheFormat);
+    for (const char* o : kCompileOptions) id += std::string("|") + o;
+    if (!sched_option(opt).empty()) id += "|-mllvm " + sched_option(opt);
+    if (slp_off(opt)) id += "|-fno-slp-vectorize";
+    int maj = 0, min = 0, rt = 0;
+    if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) id += "|hiprtc" + std::to_string(maj) + "." + std::to_string(min);
+    id += "|rtc=" + (use_helper(opt) ? helper_identity() : rtc_library());
+    if (hipRuntimeGetVersion(&rt) == hipSuccess) id += "|hip" + std::to_string(rt);
+    return id;
+}
+
+// At most this many helpers run at once (survey.prepare_survey_kernels: 16 threads): the
+// compiles are CPU work, and the GPU box's share of the host is 16 cores.
+constexpr int kMaxHelpers = 16;
 std::mutex g_helper_mu;
 std::condition_variable g_helper_cv;
 int g_helpers = 0;
@@ -457,8 +539,8 @@ int g_helpers = 0;
 // One compile in a child process (wost_jitc): source, code object and the compiler's
 // log pass through files of a private scratch directory. false (and *err) when the helper
 // could not be started or did not produce a code object; the caller then compiles here.
-bool compile_in_helper(const std::string& helper, const std::vector<std::string>& opts, const std::string& src,
-                       std::vector<char>& code, std::string* err) {
+bool compile_in_helper(const std::vector<std::string>& opts, const std::string& src, std::vector<char>& code,
+                       std::string* err) {
     {
         std::unique_lock<std::mutex> lock(g_helper_mu);
         g_helper_cv.wait(lock, [] { return g_helpers < kMaxHelpers; });
@@ -470,22 +552,13 @@ bool compile_in_helper(const std::string& helper, const std::vector<std::string>
             g_helper_cv.notify_one();
         }
     } slot;
-    const char* tmp = std::getenv("TMPDIR");
-    std::string dir = std::string(tmp && *tmp ? tmp : "/tmp") + "/wost_jitc.XXXXXX";
-    if (!mkdtemp(&dir[0])) {
+    Scratch sc;
+    if (!sc.ok) {
         *err = std::string("mkdtemp: ") + std::strerror(errno);
         return false;
     }
-    const std::string src_path = dir + "/kernel.hip", out_path = dir + "/kernel.hsaco", log_path = dir + "/log.txt";
-    struct Cleanup {
-        const std::string &d, &a, &b, &c;
-        ~Cleanup() {
-            unlink(a.c_str());
-            unlink(b.c_str());
-            unlink(c.c_str());
-            rmdir(d.c_str());
-        }
-    } cleanup{dir, src_path, out_path, log_path};
+    const std::string src_path = sc.file("kernel.hip"), out_path = sc.file("kernel.hsaco"),
+                      log_path = sc.file("log.txt"), stdout_path = sc.file("stdout.txt");
     {
         std::ofstream f(src_path, std::ios::binary);
         f.write(src.data(), (std::streamsize)src.size());
@@ -494,48 +567,27 @@ bool compile_in_helper(const std::string& helper, const std::vector<std::string>
             return false;
         }
     }
-    std::vector<std::string> args = {helper, src_path, out_path};
+    std::vector<std::string> args = {helper_path(), src_path, out_path};
     args.insert(args.end(), opts.begin(), opts.end());
-    std::vector<char*> argv;
-    for (std::string& a : args) argv.push_back(&a[0]);
-    argv.push_back(nullptr);
-    posix_spawn_file_actions_t fa;
-    posix_spawn_file_actions_init(&fa);
-    posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
-    posix_spawn_file_actions_addopen(&fa, 1, "/dev/null", O_WRONLY, 0);
-    posix_spawn_file_actions_addopen(&fa, 2, log_path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
-    pid_t pid = -1;
-    const int rc = posix_spawn(&pid, helper.c_str(), &fa, nullptr, argv.data(), environ);
-    posix_spawn_file_actions_destroy(&fa);
-    if (rc != 0) {
-        *err = std::string("posix_spawn(") + helper + "): " + std::strerror(rc);
-        return false;
-    }
-    int status = 0;
-    while (waitpid(pid, &status, 0) < 0) {
-        if (errno != EINTR) {
-            *err = std::string("waitpid: ") + std::strerror(errno);
-            return false;
-        }
-    }
-    if (WIFEXITED(status) && WEXITSTATUS(status) == 0 && read_file(out_path, code)) return true;
+    std::string how;
+    if (run_child(args, stdout_path, log_path, &how) && read_file(out_path, code)) return true;
     std::vector<char> log;
     read_file(log_path, log);
-    *err = "wost_jitc " + (WIFEXITED(status) ? "exit status " + std::to_string(WEXITSTATUS(status))
-                                             : "signal " + std::to_string(WTERMSIG(status))) +
-           ": " + std::string(log.begin(), log.end());
+    *err = "wost_jitc " + (how.empty() ? std::string("wrote no code object") : how) + ": " +
+           std::string(log.begin(), log.end());
     return false;
 }
 
-// A compile for `arch`, in the helper when there is one and opt.jit_process is set
-// (the same code object either way), else -- or when the helper failed -- in this process.
+// A compile for `arch`, in the helper when there is one and opt.jit_process is set, else
+// -- or when the helper failed -- in this process. *in_helper: where it ran (the cache key
+// names the compiler of the helper route).
 bool compile(const Options& opt, const std::string& src, const std::string& arch, std::vector<char>& code,
              std::string* err, bool* in_helper = nullptr) {
     const std::vector<std::string> opts = compile_options(opt, arch);
     if (in_helper) *in_helper = false;
-    if (opt.jit_process && !helper_path().empty()) {
+    if (use_helper(opt)) {
         std::string herr;
-        if (compile_in_helper(helper_path(), opts, src, code, &herr)) {
+        if (compile_in_helper(opts, src, code, &herr)) {
             if (in_helper) *in_helper = true;
             return true;
         }
@@ -551,7 +603,7 @@ bool jit_compile_host(const Options& opt, const std::string& source, const std::
     return compile(opt, source, arch, *code, err, in_helper);
 }
 
-bool jit_helper_available() { return !helper_path().empty(); }
+bool jit_helper_available() { return !helper_identity().empty(); }
 
 bool jit_const_dirichlet(const Options& o, int nd) { return nd <= o.const_vertices; }
 
@@ -811,10 +863,13 @@ bool jit_get_kernel(const Options& opt, int device, const std::string& source, h
 #endif
     if (dir.empty() || !read_file(dir + "/" + name, code)) {
         const auto t0 = std::chrono::steady_clock::now();
-        if (!compile(opt, source, arch, code, err)) return false;
+        bool in_helper = false;
+        if (!compile(opt, source, arch, code, err, &in_helper)) return false;
         if (compile_ms)
             *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        write_file_atomic(dir, name, code);
+        // (a helper route that fell back to this process's compiler does not fill the disk
+        // cache under the helper's compiler's key)
+        if (in_helper == use_helper(opt)) write_file_atomic(dir, name, code);
     }
     Entry e;
     if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess) {

@@ -1,6 +1,7 @@
 // wost_jitc -- libwost's compile helper: one field-specialised walk kernel per run.
 //
 //   wost_jitc <source file> <code object file> <hiprtc option>...
+//   wost_jitc --identity      (prints the hiprtc library it compiles with)
 //
 // Reads the generated source, compiles it with hiprtc and the given options against the
 // headers embedded in this binary (the same bytes as libwost's), writes the code object,
@@ -16,6 +17,10 @@
 #include "wost_rtc.h"
 
 int main(int argc, char** argv) {
+    if (argc == 2 && std::string(argv[1]) == "--identity") {
+        std::printf("%s\n", wost::rtc_library().c_str());
+        return 0;
+    }
     if (argc < 4) {
         std::fprintf(stderr, "usage: %s <source file> <code object file> <hiprtc option>...\n", argv[0]);
         return 2;

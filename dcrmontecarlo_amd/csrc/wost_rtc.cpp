@@ -1,7 +1,10 @@
 // wost_rtc.cpp -- see wost_rtc.h.
 #include "wost_rtc.h"
 
+#include <dlfcn.h>
 #include <hip/hiprtc.h>
+#include <limits.h>
+#include <stdlib.h>
 
 // Header sources embedded at build time (Makefile: wost_embedded.cpp).
 extern const char wost_embedded_wost_h[];
@@ -9,6 +12,13 @@ extern const char wost_embedded_wost_device_h[];
 extern const char wost_embedded_wost_walk_h[];
 
 namespace wost {
+
+std::string rtc_library() {
+    Dl_info info;
+    if (!dladdr(reinterpret_cast<void*>(&hiprtcCompileProgram), &info) || !info.dli_fname) return "unknown";
+    char buf[PATH_MAX];
+    return realpath(info.dli_fname, buf) ? std::string(buf) : std::string(info.dli_fname);
+}
 
 bool rtc_compile(const std::string& source, const std::vector<std::string>& options, std::vector<char>* code,
                  std::string* log) {

@@ -20,4 +20,9 @@ namespace wost {
 bool rtc_compile(const std::string& source, const std::vector<std::string>& options, std::vector<char>* code,
                  std::string* log);
 
+// The file of the hiprtc library this process compiles with (the loader may have bound
+// libwost to another copy than /opt/rocm's: PyTorch-ROCm ships its own, whose compiler is
+// another ROCm release's), part of the kernel cache key. wost_jitc --identity prints its own.
+std::string rtc_library();
+
 }  // namespace wost

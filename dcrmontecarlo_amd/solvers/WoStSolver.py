@@ -428,6 +428,20 @@ class WostSolver_2D:
             _lib.check(_lib.lib.wost_set_field(self._h, _lib.SLOT_SOURCE, ctypes.pointer(wf) if wf else None),
                        "WostSolver_2D.solve_sources")
 
+    def prepare_sources(self, sources, n_points: int):
+        """Compile (or fetch from the kernel caches) the kernel that solve_sources of
+        ``n_points`` points with these ``sources`` launches, without solving or changing the
+        handle (wost_prepare_sources). Thread-safe with other prepare_sources calls, also on
+        this solver, but not with its solves: a survey prepares every group's kernel from a
+        thread pool first, so that their compiles overlap in the compile helper."""
+        fields = self.source_fields(sources)
+        for c0 in range(0, len(fields), _lib.WOST_MAX_SOURCES):
+            chunk = fields[c0:c0 + _lib.WOST_MAX_SOURCES]
+            packed = [_lib.make_field(f) for f in chunk]
+            arr = (ctypes.POINTER(_lib.WostField) * len(chunk))(*[ctypes.pointer(wf) for wf, _ in packed])
+            _lib.check(_lib.lib.wost_prepare_sources(self._h, arr, len(chunk), int(n_points)),
+                       "WostSolver_2D.prepare_sources")
+
     def _solve_sources(self, solvePoints, sources, nWalks, maxSteps, eps, seed, want_walks):
         p = _points_np(solvePoints)
         n = p.shape[0]

@@ -575,6 +575,34 @@ def group_seed(seed: int, g: int) -> int:
     return (int(seed) * 0x9E3779B1 + g) & (2**64 - 1)
 
 
+def prepare_survey_kernels(sc, solvers, srcs, batches, key=None, max_workers: int = 16) -> int:
+    """Compile every group's field-specialised kernels before a survey's solves look them
+    up (WostSolver_2D.prepare_sources), from a pool of threads whose compiles overlap in
+    libwost's compile helper processes: a fresh process's first C5 survey compiles 34
+    kernels, which the survey's own handle threads (2 per handle pair) would otherwise
+    compile a few at a time. Group g's kernel of field f is prepared on the handle that
+    solves it. ``key`` (hashable): skip when these solvers already prepared it. Returns the
+    number of kernels prepared (0 when skipped)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    if not all(hasattr(s, "prepare_sources") for s in solvers):   # (host stand-ins)
+        return 0
+    if key is not None and all(key in getattr(s, "_prepared_surveys", ()) for s in solvers):
+        return 0
+    k = max(1, len(solvers) // 2)
+    jobs = [(solvers[2 * (g % k) + f], srcs[t0:t1], j1 - j0)
+            for g, (j0, j1, t0, t1) in enumerate(batches) for f in (0, 1)]
+    with ThreadPoolExecutor(max_workers=max(1, min(max_workers, len(jobs)))) as ex:
+        for fut in [ex.submit(s.prepare_sources, src, n) for s, src, n in jobs]:
+            fut.result()
+    if key is not None:
+        for s in solvers:
+            if not hasattr(s, "_prepared_surveys"):
+                s._prepared_surveys = set()
+            s._prepared_surveys.add(key)
+    return len(jobs)
+
+
 def _run_fields_distributed(sc, solvers, srcs, batches, n_walks, seed, comm, record, concurrent=True,
                             phase_ms: dict | None = None):
     """The model and background fields of a multi-source survey across the ranks of one
@@ -708,6 +736,9 @@ def run_wenner_survey(sc: Scenario, alpha_bg: float, n_walks: int, a: int = 1, w
         raise ValueError("solvers: (model, background) handle pairs, e.g. (model, background) or "
                          "(model, background, model2, background2)")
     k = len(solvers) // 2   # handle pairs: group g runs on pair g mod k
+    # the groups' kernels, compiled at once on a cold start (a no-op for prepared solvers)
+    prepare_survey_kernels(sc, solvers, srcs, batches,
+                           key=("wenner", a, float(width), hash(np.ascontiguousarray(sc.points).tobytes())))
 
     def record(f, g, st, local):
         j0, j1, t0, t1 = batches[g]

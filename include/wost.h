@@ -265,6 +265,14 @@ int wost_solve_history(wost_handle* h, const float* points, int64_t n_points,
  * source with the same seed. Needs the field-specialised (hiprtc) kernel when
  * S > 1. wost_solve and wost_solve_history need S == 1. */
 int wost_set_sources(wost_handle* h, const wost_field* const* sources, int32_t n_sources);
+/* Compile (or fetch from the kernel caches) the field-specialised kernel that
+ * wost_set_sources(h, sources, n_sources) and a wost_solve_multi / wost_solve_range of
+ * n_points would launch first, without changing the handle or launching anything: a survey
+ * prepares its groups' kernels from many threads at once (their compiles overlap in the
+ * compile helper, wost_jit_compile) before its solves look them up. Thread-safe with other
+ * wost_prepare_sources calls, also on the same handle; not with a solve, wost_set_sources or
+ * an option change on that handle. No reference counterpart. */
+int wost_prepare_sources(wost_handle* h, const wost_field* const* sources, int32_t n_sources, int64_t n_points);
 int wost_solve_multi(wost_handle* h, const float* points, int64_t n_points,
                      int64_t walks_per_point, int64_t block_begin, int64_t block_end,
                      int32_t max_steps, float eps, uint64_t seed,

@@ -116,3 +116,54 @@ def test_homogeneous_survey_apparent_resistivity_is_background(gpu_available):
     ok = r.background.dv != 0
     assert ok.all()
     np.testing.assert_allclose(r.rho.rho_a[ok], 100.0, rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["dcr_dipole", "wenner_topography"])
+def test_prepared_kernel_is_the_one_the_solve_launches(gpu_available, name):
+    """wost_prepare_sources (survey.prepare_survey_kernels): preparing a group's kernel
+    from several threads at once -- also on one handle -- compiles exactly the kernel its
+    solve_sources then looks up (no compile in the solve: jit_ms == 0), and the solve's
+    bits equal those of an unprepared handle's."""
+    import threading
+
+    from dcrmontecarlo_amd import scenarios as S
+
+    sc = S.ALL[name](**({"n_electrodes": 32, "n_walks": 256} if name == "wenner_topography" else {}))
+    pts = sc.points[:6]
+    W, seed = 1024, 31
+    # sources no other test compiled: a fresh kernel for this process's module cache
+    rng = np.random.default_rng()
+    srcs = _sources(sc, 4)
+    srcs = [f * float(1.0 + rng.uniform(0.01, 0.02)) for f in srcs]
+    prepared = sc.solver()
+    errs = []
+
+    def prep():
+        try:
+            prepared.prepare_sources(srcs, len(pts))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=prep) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    u, st = prepared.solve_sources(pts, srcs, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=seed,
+                                   return_stats=True)
+    assert prepared.last_timing["jit_ms"] == 0.0
+    other = sc.solver()
+    u2, st2 = other.solve_sources(pts, srcs, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=seed,
+                                  return_stats=True)
+    np.testing.assert_array_equal(np.asarray(u), np.asarray(u2))
+    np.testing.assert_array_equal(st.stderr, st2.stderr)
+
+
+def test_prepare_sources_argument_errors(gpu_available):
+    sc, s = _solver("poisson_square")
+    with pytest.raises(Exception):
+        s.prepare_sources(_sources(sc, 2), 0)
+    s.set_jit(False)
+    with pytest.raises(Exception):
+        s.prepare_sources(_sources(sc, 2), 4)

@@ -7,6 +7,8 @@ in-process compiles wait for one another (ROCm's compiler library serialises one
 process's compiles: the C5 survey's cold start)."""
 import ctypes
 import os
+import subprocess
+import sys
 import threading
 import time
 
@@ -46,15 +48,33 @@ def test_helper_is_installed_next_to_the_library():
     assert os.access(HELPER, os.X_OK), "make -C dcrmontecarlo_amd/csrc builds wost_jitc next to libwost.so"
 
 
+EQUAL = r"""
+import sys
+sys.path.insert(0, %r)
+sys.path.insert(0, %r)
+import test_jit_helper as T
+from dcrmontecarlo_amd import scenarios as S
+src = S.dcr_dipole().kernel_source() if sys.argv[1] == "dcr_dipole" else T._survey_source()
+rc_h, code_h, used_h = T.compile_source(src, in_process=False)
+rc_i, code_i, used_i = T.compile_source(src, in_process=True)
+assert rc_h == 0 and rc_i == 0
+assert used_h == 1 and used_i == 0
+assert len(code_h) > 1000 and code_h[:4] == b"\x7fELF"
+print("equal" if code_h == code_i else "differ", len(code_h), len(code_i))
+"""
+
+
 @pytest.mark.parametrize("which", ["dcr_dipole", "wenner_survey_group"])
-def test_helper_code_object_equals_in_process(which):
-    src = S.dcr_dipole().kernel_source() if which == "dcr_dipole" else _survey_source()
-    rc_h, code_h, used_h = compile_source(src, in_process=False)
-    rc_i, code_i, used_i = compile_source(src, in_process=True)
-    assert rc_h == 0 and rc_i == 0, _lib.lib.wost_last_error()
-    assert used_h == 1 and used_i == 0
-    assert len(code_h) > 1000 and code_h[:4] == b"\x7fELF"
-    assert code_h == code_i
+def test_helper_code_object_equals_in_process(which, tmp_path):
+    # in a fresh process that has not imported PyTorch: libwost then binds /opt/rocm's
+    # hiprtc, the helper's compiler (PyTorch-ROCm's own copy is another ROCm release's,
+    # which the kernel cache key tells apart: wost_jit.cpp cache_identity)
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, AMD_COMGR_CACHE_DIR=str(tmp_path / "comgr"))
+    out = subprocess.run([sys.executable, "-c", EQUAL % (os.path.dirname(here), here), which], env=env,
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert out.stdout.split()[0] == "equal", out.stdout
 
 
 def test_a_source_that_does_not_compile_reports_the_compiler():

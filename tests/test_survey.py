@@ -198,6 +198,44 @@ def test_wenner_survey_bookkeeping_one_gpu(E, a):
     # protocol over thread ranks in tests/test_survey_distributed.py
 
 
+class _PreparingSolver(_FakeSolver):
+    """A stand-in that also records wost_prepare_sources calls (from the prepare pool)."""
+
+    def __init__(self, scale, log, name):
+        super().__init__(scale)
+        self.log, self.name = log, name
+
+    def prepare_sources(self, srcs, n_points):
+        k = tuple(float(np.asarray(s(np.array([0.0, -50.0])))) for s in srcs)
+        self.log.append((self.name, k, n_points))
+
+
+def test_wenner_survey_prepares_every_group_kernel_once():
+    """survey.prepare_survey_kernels: before the first survey's solves, every group's kernel
+    of each field is prepared on the handle that solves it (group g on pair g mod k), with
+    the group's transmitters and electrode count; a second survey on the same solvers
+    prepares nothing."""
+    E = 40
+    sc = S.wenner_topography(n_electrodes=E, n_walks=8, n_segments=100)
+    log = []
+    sv = (_PreparingSolver(1.0, log, "m0"), _PreparingSolver(0.5, log, "h0"),
+          _PreparingSolver(1.0, log, "m1"), _PreparingSolver(0.5, log, "h1"))
+    survey.run_wenner_survey(sc, 1e-2, 8, seed=3, solvers=sv)
+    groups = list(survey.wenner_batches(E, 1))
+    srcs = [survey.dipole_source(sc.points[q], sc.points[q + 3], 0.5) for q in range(E - 3)]
+    want = set()
+    for g, (j0, j1, t0, t1) in enumerate(groups):
+        k = tuple(float(np.asarray(s(np.array([0.0, -50.0])))) for s in srcs[t0:t1])
+        for f, name in enumerate(("m", "h")):
+            want.add((f"{name}{g % 2}", k, j1 - j0))
+    assert len(log) == 2 * len(groups) and set(log) == want
+    survey.run_wenner_survey(sc, 1e-2, 8, seed=4, solvers=sv)
+    assert len(log) == 2 * len(groups)                              # already prepared
+    sc2 = S.wenner_topography(n_electrodes=E - 4, n_walks=8, n_segments=100)
+    survey.run_wenner_survey(sc2, 1e-2, 8, seed=4, solvers=sv)     # other electrodes: prepared again
+    assert len(log) == 2 * len(groups) + 2 * len(list(survey.wenner_batches(E - 4, 1)))
+
+
 def test_apparent_resistivity_resolves_only_with_the_model_error_small():
     """resolved needs the model's dV resolved too (round-2 verdict): a precise background
     with a model dV inside its own noise is not a resolved rho_a."""
