@@ -513,6 +513,20 @@ const std::string& helper_identity() {
 
 bool use_helper(const Options& opt) { return opt.jit_process != 0 && !helper_identity().empty(); }
 
+const std::string& rtc_library_once() {
+    static const std::string lib = rtc_library();
+    return lib;
+}
+
+enum class Route { kAuto, kHelper, kInProcess };
+
+// The compiler a handle's compile uses: its option jit_process with a usable helper
+// routes through the helper's compiler, else this process's.
+const std::string& route_compiler(const Options& opt) {
+    return use_helper(opt) ? helper_identity() : rtc_library_once();
+}
+
+
 // The cache key's compile identity: the format, the compile options, the compiler -- the
 // hiprtc library that compiles (the helper's, or the one this process bound: a process that
 // imported PyTorch-ROCm first binds PyTorch's own copy, another ROCm release's compiler) --
@@ -524,7 +538,7 @@ std::string cache_identity(const Options& opt) {
     if (slp_off(opt)) id += "|-fno-slp-vectorize";
     int maj = 0, min = 0, rt = 0;
     if (hiprtcVersion(&maj, &min) == HIPRTC_SUCCESS) id += "|hiprtc" + std::to_string(maj) + "." + std::to_string(min);
-    id += "|rtc=" + (use_helper(opt) ? helper_identity() : rtc_library());
+    id += "|rtc=" + route_compiler(opt);
     if (hipRuntimeGetVersion(&rt) == hipSuccess) id += "|hip" + std::to_string(rt);
     return id;
 }
@@ -578,21 +592,37 @@ bool compile_in_helper(const std::vector<std::string>& opts, const std::string& 
     return false;
 }
 
-// A compile for `arch`, in the helper when there is one and opt.jit_process is set, else
-// -- or when the helper failed -- in this process. *in_helper: where it ran (the cache key
-// names the compiler of the helper route).
-bool compile(const Options& opt, const std::string& src, const std::string& arch, std::vector<char>& code,
-             std::string* err, bool* in_helper = nullptr) {
+std::mutex g_inproc_mu;   // at most one compile in this process (comgr serialises them anyway)
+
+// A compile for `arch`. kAuto (handles with jit_process): in this process when no other
+// compile runs here and this process binds the helper's compiler (a lone compile saves the
+// child's start, ~25 ms), else in a helper, so that concurrent compiles overlap; kHelper:
+// in a helper; kInProcess: here. A helper that fails falls back to this process.
+// *compiler: the hiprtc library that compiled (the disk cache only takes code of the
+// compiler its key names).
+bool compile(const Options& opt, Route route, const std::string& src, const std::string& arch,
+             std::vector<char>& code, std::string* err, std::string* compiler, bool* in_helper) {
     const std::vector<std::string> opts = compile_options(opt, arch);
-    if (in_helper) *in_helper = false;
-    if (use_helper(opt)) {
+    *in_helper = false;
+    const bool helper = route != Route::kInProcess && !helper_identity().empty();
+    if (helper && route == Route::kAuto && helper_identity() == rtc_library_once()) {
+        std::unique_lock<std::mutex> lock(g_inproc_mu, std::try_to_lock);
+        if (lock.owns_lock()) {
+            *compiler = rtc_library_once();
+            return rtc_compile(src, opts, &code, err);
+        }
+    }
+    if (helper) {
         std::string herr;
         if (compile_in_helper(opts, src, code, &herr)) {
-            if (in_helper) *in_helper = true;
+            *compiler = helper_identity();
+            *in_helper = true;
             return true;
         }
         std::fprintf(stderr, "libwost: compile helper failed, compiling in this process: %s\n", herr.c_str());
     }
+    std::lock_guard<std::mutex> lock(g_inproc_mu);
+    *compiler = rtc_library_once();
     return rtc_compile(src, opts, &code, err);
 }
 
@@ -600,7 +630,9 @@ bool compile(const Options& opt, const std::string& src, const std::string& arch
 
 bool jit_compile_host(const Options& opt, const std::string& source, const std::string& arch,
                       std::vector<char>* code, std::string* err, bool* in_helper) {
-    return compile(opt, source, arch, *code, err, in_helper);
+    std::string compiler;
+    return compile(opt, opt.jit_process ? Route::kHelper : Route::kInProcess, source, arch, *code, err, &compiler,
+                   in_helper);
 }
 
 bool jit_helper_available() { return !helper_identity().empty(); }
@@ -864,12 +896,15 @@ bool jit_get_kernel(const Options& opt, int device, const std::string& source, h
     if (dir.empty() || !read_file(dir + "/" + name, code)) {
         const auto t0 = std::chrono::steady_clock::now();
         bool in_helper = false;
-        if (!compile(opt, source, arch, code, err, &in_helper)) return false;
+        std::string compiler;
+        if (!compile(opt, opt.jit_process ? Route::kAuto : Route::kInProcess, source, arch, code, err, &compiler,
+                     &in_helper))
+            return false;
         if (compile_ms)
             *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        // (a helper route that fell back to this process's compiler does not fill the disk
-        // cache under the helper's compiler's key)
-        if (in_helper == use_helper(opt)) write_file_atomic(dir, name, code);
+        // (a helper route that fell back to another compiler does not fill the disk cache
+        // under the key of the helper's)
+        if (compiler == route_compiler(opt)) write_file_atomic(dir, name, code);
     }
     Entry e;
     if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess) {
