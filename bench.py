@@ -504,9 +504,16 @@ def main():
     for k in range(args.warmup):
         ts = time.perf_counter()
         t = one_step(1000 + k)
-        if k == 0:   # the process's first solve: hiprtc compiles the kernel (empty cache)
+        if k == 0:   # the process's first solve: its kernel is in no cache (empty WOST_JIT_CACHE)
+            # (option jit_race: the compile runs in a helper process while the precompiled
+            # kernel starts the walks; jit_compile_ms is then 0)
             cold["first_handle"] = {"first_solve_ms": 1e3 * (time.perf_counter() - ts),
-                                    "jit_compile_ms": float(t["jit_ms"]), "walk_kernel_ms": float(t["walk_kernel_ms"])}
+                                    "jit_compile_ms": float(t["jit_ms"]), "walk_kernel_ms": float(t["walk_kernel_ms"]),
+                                    "precompiled_walks": int(t["precompiled_walks"]),
+                                    "walks": int(t["total_walks"])}
+        elif k == 1:   # the second: waits for the rest of that compile, if any
+            cold["first_handle"].update({"second_solve_ms": 1e3 * (time.perf_counter() - ts),
+                                         "second_jit_wait_ms": float(t["jit_ms"])})
     libinfo = library_check([solver])
 
     barrier_sync()
@@ -824,12 +831,17 @@ def wenner_main(args, world, rank, local):
                 ts = time.perf_counter()
                 _, st = sv.solve(sc.points[:nb], nWalks=2048, maxSteps=sc.max_steps, eps=sc.eps, seed=5,
                                  return_stats=True)
-                first = (1e3 * (time.perf_counter() - ts), st.kernel_ms, sv.last_timing["jit_ms"])
-                if tree:   # the single launch, warm: a second solve on the same (now warm) handle
-                    _, st = sv.solve(sc.points[:nb], nWalks=2048, maxSteps=sc.max_steps, eps=sc.eps, seed=5,
-                                     return_stats=True)
+                first = (1e3 * (time.perf_counter() - ts), st.kernel_ms, sv.last_timing["jit_ms"],
+                         int(sv.last_timing["precompiled_walks"]))
+                # the rate of the warm single launch: a second solve on the same handle (the
+                # first may have run on the precompiled kernel while its own compiled: jit_race)
+                _, st = sv.solve(sc.points[:nb], nWalks=2048, maxSteps=sc.max_steps, eps=sc.eps, seed=5,
+                                 return_stats=True)
+                if tree:
                     cold["tree_single_launch"] = {"first_solve_ms": first[0], "first_walk_kernel_ms": first[1],
-                                                  "first_jit_ms": first[2], "second_walk_kernel_ms": st.kernel_ms,
+                                                  "first_jit_ms": first[2], "first_precompiled_walks": first[3],
+                                                  "second_walk_kernel_ms": st.kernel_ms,
+                                                  "second_jit_wait_ms": sv.last_timing["jit_ms"],
                                                   "first_over_second_kernel": first[1] / st.kernel_ms}
                 rates[tree] = st.total_steps / (st.kernel_ms * 1e-3)
             bs = perfmodel.flops_per_step(sc)      # SURVEY 8d v1, brute force (~290,000 FLOP/step)

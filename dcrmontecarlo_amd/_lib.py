@@ -22,7 +22,7 @@ WOST_ERR_UNSUPPORTED = -4
 WOST_ERR_OOM = -5
 WOST_ERR_COMM = -6
 
-ABI_VERSION = 5   # include/wost.h WOST_ABI_VERSION
+ABI_VERSION = 6   # include/wost.h WOST_ABI_VERSION
 WOST_COMM_ID_BYTES = 128
 WOST_COMM_SUM, WOST_COMM_MAX = 0, 1
 WOST_BLOCK_WALKS = 4096
@@ -68,7 +68,7 @@ class WostTiming(ctypes.Structure):
                 ("blocks_per_cu", c_int32), ("block_threads", c_int32), ("chunk0", c_int32), ("chunk", c_int32),
                 ("adaptive", c_int32), ("max_walk_steps", c_uint32), ("jit_ms", c_double), ("span_ms", c_double),
                 ("tail_ms", c_double), ("last_wave_ms", c_double), ("last_wave_iters", c_uint32),
-                ("max_wave_iters", c_uint32)]
+                ("max_wave_iters", c_uint32), ("precompiled_walks", c_uint64)]
 
 
 class WostDistTiming(ctypes.Structure):

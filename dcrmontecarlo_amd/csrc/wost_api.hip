@@ -302,14 +302,39 @@ int jit_source(const wost_handle* h, const Program& prog, int mode, bool record,
     return WOST_OK;
 }
 
+// The handle's key of a kernel variant: everything its source depends on besides the
+// program (prog_version): the staging level, the exact workgroup size (a multiple of 64,
+// at most 1024) and the trig choice
+int jit_key(const wost_handle* h, int mode, bool record, int ns, int block, bool global_polylines, int tree_stage) {
+    const bool exact = exact_trig_of(h);
+    return (((((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 3 + tree_stage) * 17 + block / 64) * 2 +
+            (global_polylines ? 1 : 0)) * 2 + (exact ? 1 : 0);
+}
+
+// jit_kernel without blocking on a compile (option jit_race): kReady with the handle's
+// kernel set, kStarted when its compile began now in the background (ticket), else kWait.
+JitTry jit_kernel_try(wost_handle* h, int mode, int block, bool global_polylines, int tree_stage, JitTicket* ticket) {
+    if (!h->jit_enabled) return JitTry::kWait;
+    const int key = jit_key(h, mode, false, 1, block, global_polylines, tree_stage);
+    if (h->jit_mode == key && h->jit_version == h->prog_version && h->jit_fn) return JitTry::kReady;
+    std::string src, err;
+    if (jit_source(h, h->prog, mode, false, 1, block, global_polylines, tree_stage, &src) != WOST_OK)
+        return JitTry::kWait;
+    hipFunction_t fn = nullptr, afn = nullptr;
+    const JitTry r = jit_try_kernel(h->opt, h->device, src, &fn, &afn, ticket, &err);
+    if (r == JitTry::kReady && (!mode_delta(mode) || afn)) {
+        h->jit_mode = key;
+        h->jit_version = h->prog_version;
+        h->jit_fn = fn;
+        h->jit_alpha_fn = afn;
+    }
+    return r;
+}
+
 hipFunction_t jit_kernel(wost_handle* h, int mode, bool record, int ns = 1, int block = kWalkBlock,
                          bool global_polylines = false, int tree_stage = 0, double* compile_ms = nullptr) {
     if (!h->jit_enabled) return nullptr;
-    // the cache key holds everything the source depends on: the staging level, the
-    // exact workgroup size (a multiple of 64, at most 1024) and the trig choice
-    const bool exact = exact_trig_of(h);
-    const int key = (((((2 * mode + (record ? 1 : 0)) * (WOST_MAX_SOURCES + 1) + ns) * 3 + tree_stage) * 17 +
-                      block / 64) * 2 + (global_polylines ? 1 : 0)) * 2 + (exact ? 1 : 0);
+    const int key = jit_key(h, mode, record, ns, block, global_polylines, tree_stage);
     if (h->jit_mode == key && h->jit_version == h->prog_version) return h->jit_fn;
     h->jit_fn = nullptr;
     h->jit_alpha_fn = nullptr;
@@ -1337,6 +1362,120 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     return WOST_OK;
 }
 
+// Accumulates a piece's timing into a multi-launch solve's (wost_solve_range, solve_race).
+void add_timing(wost_timing& acc, const wost_timing& t) {
+    acc.walk_kernel_ms += t.walk_kernel_ms;
+    acc.reduce_kernel_ms += t.reduce_kernel_ms;
+    acc.total_ms += t.total_ms;
+    acc.n_launches += t.n_launches;
+    acc.total_steps += t.total_steps;
+    acc.total_walks += t.total_walks;
+    acc.grid_blocks = t.grid_blocks;
+    acc.jit = t.jit;
+    acc.tree = t.tree;
+    acc.blocks_per_cu = t.blocks_per_cu;
+    acc.block_threads = t.block_threads;
+    acc.chunk0 = t.chunk0;
+    acc.chunk = t.chunk;
+    acc.adaptive = t.adaptive;
+    acc.max_walk_steps = std::max(acc.max_walk_steps, t.max_walk_steps);
+    acc.jit_ms += t.jit_ms;
+    acc.span_ms += t.span_ms;
+    acc.tail_ms = t.tail_ms;
+    acc.last_wave_ms = t.last_wave_ms;
+    acc.last_wave_iters = t.last_wave_iters;
+    acc.max_wave_iters = std::max(acc.max_wave_iters, t.max_wave_iters);
+    acc.precompiled_walks += t.precompiled_walks;
+}
+
+// A whole single-source solve whose field-specialised kernel is in no cache (option
+// jit_race; the reference calls solve() once per script): its compile starts in a helper
+// process, and meanwhile the precompiled kernel -- the same bits walk for walk
+// (test_jit_kernel_matches_interpreted_kernel) but 2-5x slower -- runs the walks in ranges
+// of every point (the first ~2^19 walks, then ~16 ms of work each); once the compile is
+// done the specialised kernel runs the rest. Ranges of walks are whole blocks, so the
+// block sums, their order and every output are those of one launch (as wost_solve_range's).
+// A solve that finds the compile already running waits for it instead (jit_get_kernel).
+int solve_race(wost_handle* h, const float* points, int64_t n_points, int64_t W, int32_t max_steps, float eps,
+               uint64_t seed, double* block_stats, double* point_stats, float* walk_values, uint32_t* walk_steps) {
+    const int64_t nb = wost_num_blocks(n_points, W);
+    auto plain = [&]() {
+        return solve_impl(h, points, n_points, W, 0, nb, max_steps, eps, seed, block_stats, point_stats, walk_values,
+                          walk_steps, nullptr);
+    };
+    if (!points) return plain();
+    for (int64_t i = 0; i < 2 * n_points; ++i)
+        if (!std::isfinite(points[i])) return plain();   // (its error message)
+    const int mode = walk_mode(h);
+    if (mode_delta(mode) && !h->fields[SLOT_F].present) return plain();
+    HIP_TRY(hipSetDevice(h->device));
+    int rc;
+    if ((rc = upload_program(h)) != WOST_OK) return rc;
+    if (mode_tree(mode) && (rc = ensure_tree(h)) != WOST_OK) return rc;
+    KernelShape ks;
+    if ((rc = first_kernel_shape(h, mode, n_points, &ks)) != WOST_OK) return rc;
+    JitTicket ticket;
+    const int stage = ks.tree_lds > 0 ? (ks.tree_verts > 0 ? 2 : 1) : 0;
+    if (jit_kernel_try(h, mode, ks.block, ks.gpoly, stage, &ticket) != JitTry::kStarted) return plain();
+
+    const int row = 3;
+    const int64_t nbpp = (W + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
+    const int64_t max_piece = kMaxBatchWalks / WOST_BLOCK_WALKS * WOST_BLOCK_WALKS;   // walks of a point per launch
+    auto blocks_up = [](double walks) {
+        const double b = std::ceil(std::max(walks, 1.0) / WOST_BLOCK_WALKS);
+        return (int64_t)std::min(b, 1e15) * WOST_BLOCK_WALKS;
+    };
+    int64_t piece = std::min(max_piece, blocks_up((double)(1 << 19) / (double)n_points));
+    std::vector<double> all((size_t)n_points * nbpp * row), part;
+    std::vector<float> pv;
+    std::vector<uint32_t> ps;
+    wost_timing acc{};
+    bool jit_now = false;
+    const bool saved = h->jit_enabled;
+    for (int64_t w0 = 0; w0 < W;) {
+        if (!jit_now && ticket.done()) jit_now = true;
+        const int64_t w1 = std::min(W, w0 + (jit_now ? max_piece : piece));
+        const int64_t wc = w1 - w0, nbc = (wc + WOST_BLOCK_WALKS - 1) / WOST_BLOCK_WALKS;
+        part.resize((size_t)n_points * nbc * row);
+        if (walk_values) pv.resize((size_t)n_points * wc);
+        if (walk_steps) ps.resize((size_t)n_points * wc);
+        h->jit_enabled = jit_now;
+        const auto t0 = std::chrono::steady_clock::now();
+        rc = solve_impl(h, points, n_points, W, 0, 0, max_steps, eps, seed, part.data(), nullptr,
+                        walk_values ? pv.data() : nullptr, walk_steps ? ps.data() : nullptr, nullptr, false, w0, w1);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        h->jit_enabled = saved;
+        if (rc == WOST_ERR_UNSUPPORTED && !jit_now) {   // (a shape only the specialised kernel runs)
+            jit_now = true;
+            continue;
+        }
+        if (rc != WOST_OK) return rc;
+        const int64_t boff = w0 / WOST_BLOCK_WALKS;
+        for (int64_t p = 0; p < n_points; ++p) {
+            std::memcpy(&all[((size_t)p * nbpp + boff) * row], &part[(size_t)p * nbc * row], sizeof(double) * nbc * row);
+            if (walk_values) std::memcpy(walk_values + (size_t)p * W + w0, &pv[(size_t)p * wc], sizeof(float) * wc);
+            if (walk_steps) std::memcpy(walk_steps + (size_t)p * W + w0, &ps[(size_t)p * wc], sizeof(uint32_t) * wc);
+        }
+        if (!jit_now) {
+            h->timing.precompiled_walks = (uint64_t)(n_points * wc);
+            // the next range: ~16 ms of work at this one's rate, at most 8x larger
+            piece = std::min(max_piece, std::max(piece, std::min(8 * piece, blocks_up((double)wc * 16.0 / std::max(ms, 0.05)))));
+        }
+        add_timing(acc, h->timing);
+        w0 = w1;
+    }
+    if (block_stats) std::memcpy(block_stats, all.data(), sizeof(double) * all.size());
+    if (point_stats) {
+        std::fill(point_stats, point_stats + (size_t)row * n_points, 0.0);
+        for (int64_t p = 0; p < n_points; ++p)
+            for (int64_t b = 0; b < nbpp; ++b)
+                for (int c = 0; c < row; ++c) point_stats[(size_t)row * p + c] += all[((size_t)p * nbpp + b) * row + c];
+    }
+    acc.jit = jit_now ? 1 : 0;
+    h->timing = acc;
+    return WOST_OK;
+}
+
 // The handle's fields with sources[0..n) in the source slots (wost_set_sources' conversion).
 int fields_with_sources(const wost_handle* h, const wost_field* const* sources, int32_t n, HostField* out) {
     if (n < 1 || n > WOST_MAX_SOURCES || !sources)
@@ -1370,6 +1509,12 @@ extern "C" {
 int wost_solve(wost_handle* h, const float* points, int64_t n_points, int64_t W,
                int64_t block_begin, int64_t block_end, int32_t max_steps, float eps, uint64_t seed,
                double* block_stats, double* point_stats, float* walk_values, uint32_t* walk_steps) {
+    // a whole single-source solve may start on the precompiled kernel while its specialised
+    // one compiles (solve_race)
+    if (h && h->jit_enabled && h->opt.jit_race && h->n_sources == 1 && n_points > 0 && W > 0 && block_begin == 0 &&
+        block_end == wost_num_blocks(n_points, W) && max_steps >= 0 && eps == eps)
+        return solve_race(h, points, n_points, W, max_steps, eps, seed, block_stats, point_stats, walk_values,
+                          walk_steps);
     return solve_impl(h, points, n_points, W, block_begin, block_end, max_steps, eps, seed, block_stats,
                       point_stats, walk_values, walk_steps, nullptr);
 }
@@ -1414,27 +1559,7 @@ int wost_solve_range(wost_handle* h, const float* points, int64_t n_points, int6
                 std::memcpy(walk_values + ((size_t)p * Wr + woff) * ns, &pv[(size_t)p * wc * ns], sizeof(float) * wc * ns);
             if (walk_steps) std::memcpy(walk_steps + (size_t)p * Wr + woff, &ps[(size_t)p * wc], sizeof(uint32_t) * wc);
         }
-        acc.walk_kernel_ms += h->timing.walk_kernel_ms;
-        acc.reduce_kernel_ms += h->timing.reduce_kernel_ms;
-        acc.total_ms += h->timing.total_ms;
-        acc.n_launches += h->timing.n_launches;
-        acc.total_steps += h->timing.total_steps;
-        acc.total_walks += h->timing.total_walks;
-        acc.grid_blocks = h->timing.grid_blocks;
-        acc.jit = h->timing.jit;
-        acc.tree = h->timing.tree;
-        acc.blocks_per_cu = h->timing.blocks_per_cu;
-        acc.block_threads = h->timing.block_threads;
-        acc.chunk0 = h->timing.chunk0;
-        acc.chunk = h->timing.chunk;
-        acc.adaptive = h->timing.adaptive;
-        acc.max_walk_steps = std::max(acc.max_walk_steps, h->timing.max_walk_steps);
-        acc.jit_ms += h->timing.jit_ms;
-        acc.span_ms += h->timing.span_ms;
-        acc.tail_ms = h->timing.tail_ms;
-        acc.last_wave_ms = h->timing.last_wave_ms;
-        acc.last_wave_iters = h->timing.last_wave_iters;
-        acc.max_wave_iters = std::max(acc.max_wave_iters, h->timing.max_wave_iters);
+        add_timing(acc, h->timing);
     }
     if (block_stats) std::memcpy(block_stats, all.data(), sizeof(double) * all.size());
     if (point_stats) {

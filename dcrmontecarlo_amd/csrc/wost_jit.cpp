@@ -354,11 +354,34 @@ std::string cache_dir() {
     return "";
 }
 
+// File I/O by system calls only: a background compile's thread (jit_try_kernel) may still
+// run while the process exits and its C++ runtime's statics are torn down.
 bool read_file(const std::string& path, std::vector<char>& out) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return false;
-    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return false;
+    out.clear();
+    char buf[1 << 16];
+    for (;;) {
+        const ssize_t n = read(fd, buf, sizeof(buf));
+        if (n < 0 && errno == EINTR) continue;
+        if (n <= 0) break;
+        out.insert(out.end(), buf, buf + n);
+    }
+    close(fd);
     return !out.empty();
+}
+
+bool write_file(const std::string& path, const char* data, size_t size) {
+    const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) return false;
+    size_t done = 0;
+    while (done < size) {
+        const ssize_t n = write(fd, data + done, size - done);
+        if (n < 0 && errno == EINTR) continue;
+        if (n <= 0) break;
+        done += (size_t)n;
+    }
+    return close(fd) == 0 && done == size;
 }
 
 void write_file_atomic(const std::string& dir, const std::string& name, const std::vector<char>& data) {
@@ -373,13 +396,8 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
     // (the thread too: two threads of one process may compile the same kernel at once)
     std::string tmp = dir + "/" + name + ".tmp." + std::to_string(getpid()) + "." +
                       std::to_string(std::hash<std::thread::id>{}(std::this_thread::get_id()));
-    {
-        std::ofstream f(tmp, std::ios::binary);
-        if (!f) return;
-        f.write(data.data(), (std::streamsize)data.size());
-        if (!f) return;
-    }
-    std::rename(tmp.c_str(), (dir + "/" + name).c_str());
+    if (write_file(tmp, data.data(), data.size())) std::rename(tmp.c_str(), (dir + "/" + name).c_str());
+    else unlink(tmp.c_str());
 }
 
 struct Entry {
@@ -545,16 +563,17 @@ std::string cache_identity(const Options& opt) {
 
 // At most this many helpers run at once (survey.prepare_survey_kernels: 16 threads): the
 // compiles are CPU work, and the GPU box's share of the host is 16 cores.
+// (never destroyed: a background compile's thread may outlive the process's statics)
 constexpr int kMaxHelpers = 16;
-std::mutex g_helper_mu;
-std::condition_variable g_helper_cv;
+std::mutex& g_helper_mu = *new std::mutex;
+std::condition_variable& g_helper_cv = *new std::condition_variable;
 int g_helpers = 0;
 
 // One compile in a child process (wost_jitc): source, code object and the compiler's
 // log pass through files of a private scratch directory. false (and *err) when the helper
 // could not be started or did not produce a code object; the caller then compiles here.
-bool compile_in_helper(const std::vector<std::string>& opts, const std::string& src, std::vector<char>& code,
-                       std::string* err) {
+bool compile_in_helper(const std::string& helper, const std::vector<std::string>& opts, const std::string& src,
+                       std::vector<char>& code, std::string* err) {
     {
         std::unique_lock<std::mutex> lock(g_helper_mu);
         g_helper_cv.wait(lock, [] { return g_helpers < kMaxHelpers; });
@@ -573,15 +592,12 @@ bool compile_in_helper(const std::vector<std::string>& opts, const std::string& 
     }
     const std::string src_path = sc.file("kernel.hip"), out_path = sc.file("kernel.hsaco"),
                       log_path = sc.file("log.txt"), stdout_path = sc.file("stdout.txt");
-    {
-        std::ofstream f(src_path, std::ios::binary);
-        f.write(src.data(), (std::streamsize)src.size());
-        if (!f) {
-            *err = "cannot write " + src_path;
-            return false;
-        }
+    if (!write_file(src_path, src.data(), src.size())) {
+        *err = "cannot write " + src_path;
+        return false;
     }
-    std::vector<std::string> args = {helper_path(), src_path, out_path};
+    // (--parent: a helper whose parent has exited removes its scratch directory itself)
+    std::vector<std::string> args = {helper, "--parent=" + std::to_string(getpid()), src_path, out_path};
     args.insert(args.end(), opts.begin(), opts.end());
     std::string how;
     if (run_child(args, stdout_path, log_path, &how) && read_file(out_path, code)) return true;
@@ -614,7 +630,7 @@ bool compile(const Options& opt, Route route, const std::string& src, const std:
     }
     if (helper) {
         std::string herr;
-        if (compile_in_helper(opts, src, code, &herr)) {
+        if (compile_in_helper(helper_path(), opts, src, code, &herr)) {
             *compiler = helper_identity();
             *in_helper = true;
             return true;
@@ -855,57 +871,61 @@ std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, cons
     return o.str();
 }
 
-bool jit_get_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn, std::string* err,
-                    hipFunction_t* alpha_fn, double* compile_ms) {
-    if (compile_ms) *compile_ms = 0.0;
+namespace {
+
+// Background compiles (jit_try_kernel): one record per kernel key, written by a detached
+// thread that waits for the compile helper. The records and their lock are never freed:
+// the thread may still run while the process exits.
+struct Pending {
+    int state = 0;   // 0 compiling, 1 done (code), 2 failed
+    std::vector<char> code;
+};
+std::mutex& g_pend_mu = *new std::mutex;
+std::condition_variable& g_pend_cv = *new std::condition_variable;
+std::map<std::string, Pending*>& g_pending = *new std::map<std::string, Pending*>;
+
+struct KeyInfo {
+    std::string arch, key, name, dir;
+};
+
+bool key_of(const Options& opt, int device, const std::string& source, KeyInfo* k, std::string* err) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
         *err = "hipGetDeviceProperties failed";
         return false;
     }
-    std::string arch = prop.gcnArchName;
-    arch = arch.substr(0, arch.find(':'));
+    k->arch = prop.gcnArchName;
+    k->arch = k->arch.substr(0, k->arch.find(':'));
     // the embedded headers, compile options and compiler/runtime versions are part of the
     // key: a rebuilt library, other options or a ROCm upgrade never reuse stale code
     const std::string ident = cache_identity(opt);
-    const uint64_t h = fnv1a(source + "|" + arch + "|" + ident + "|" + wost_embedded_wost_h +
+    const uint64_t h = fnv1a(source + "|" + k->arch + "|" + ident + "|" + wost_embedded_wost_h +
                              wost_embedded_wost_device_h + wost_embedded_wost_walk_h);
     char hex[32];
     std::snprintf(hex, sizeof(hex), "%016llx", (unsigned long long)h);
-    const std::string key = std::to_string(device) + ":" + arch + ":" + hex;
-
-    {   // the in-memory cache (the lock is not held during a compile: the handles of a survey's
-        // concurrent threads compile their kernels at once -- hiprtc is thread-safe)
-        std::lock_guard<std::mutex> lock(g_mu);
-        auto it = g_modules.find(key);
-        if (it != g_modules.end()) {
-            *fn = it->second.fn;
-            if (alpha_fn) *alpha_fn = it->second.alpha_fn;
-            return true;
-        }
-    }
-    std::vector<char> code;
-    const std::string dir = cache_dir();
-    const std::string name = std::string("walk_") + arch + "_" + hex + ".hsaco";
+    k->key = std::to_string(device) + ":" + k->arch + ":" + hex;
+    k->name = std::string("walk_") + k->arch + "_" + hex + ".hsaco";
+    k->dir = cache_dir();
 #if defined(WOST_STUDY)
     if (const char* dump = std::getenv("WOST_JIT_DUMP")) {   // generated source, for offline ISA study
         const std::string s(source);
         write_file_atomic(dump, std::string("walk_") + hex + ".hip", std::vector<char>(s.begin(), s.end()));
     }
 #endif
-    if (dir.empty() || !read_file(dir + "/" + name, code)) {
-        const auto t0 = std::chrono::steady_clock::now();
-        bool in_helper = false;
-        std::string compiler;
-        if (!compile(opt, opt.jit_process ? Route::kAuto : Route::kInProcess, source, arch, code, err, &compiler,
-                     &in_helper))
-            return false;
-        if (compile_ms)
-            *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        // (a helper route that fell back to another compiler does not fill the disk cache
-        // under the key of the helper's)
-        if (compiler == route_compiler(opt)) write_file_atomic(dir, name, code);
-    }
+    return true;
+}
+
+bool memory_lookup(const std::string& key, hipFunction_t* fn, hipFunction_t* alpha_fn) {
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_modules.find(key);
+    if (it == g_modules.end()) return false;
+    *fn = it->second.fn;
+    if (alpha_fn) *alpha_fn = it->second.alpha_fn;
+    return true;
+}
+
+bool load_module(const std::string& key, const std::vector<char>& code, hipFunction_t* fn, hipFunction_t* alpha_fn,
+                 std::string* err) {
     Entry e;
     if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess) {
         *err = "hipModuleLoadData failed";
@@ -928,6 +948,99 @@ bool jit_get_kernel(const Options& opt, int device, const std::string& source, h
     *fn = e.fn;
     if (alpha_fn) *alpha_fn = e.alpha_fn;
     return true;
+}
+
+// A finished background compile's code object (state 1), copied out; blocks while one
+// runs when `wait`. Returns its state (-1: none).
+int pending_code(const std::string& key, bool wait, std::vector<char>* code) {
+    std::unique_lock<std::mutex> lock(g_pend_mu);
+    auto it = g_pending.find(key);
+    if (it == g_pending.end()) return -1;
+    Pending* p = it->second;
+    if (wait) g_pend_cv.wait(lock, [p] { return p->state != 0; });
+    if (p->state == 1) *code = p->code;
+    return p->state;
+}
+
+}  // namespace
+
+bool JitTicket::done() const {
+    if (!p) return true;
+    std::lock_guard<std::mutex> lock(g_pend_mu);
+    return static_cast<const Pending*>(p)->state != 0;
+}
+
+bool jit_get_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn, std::string* err,
+                    hipFunction_t* alpha_fn, double* compile_ms) {
+    if (compile_ms) *compile_ms = 0.0;
+    KeyInfo k;
+    if (!key_of(opt, device, source, &k, err)) return false;
+    // the in-memory cache (the lock is not held during a compile: the handles of a survey's
+    // concurrent threads compile their kernels at once)
+    if (memory_lookup(k.key, fn, alpha_fn)) return true;
+    std::vector<char> code;
+    const auto t0 = std::chrono::steady_clock::now();
+    // a background compile of it (jit_try_kernel): wait for its code object
+    if (pending_code(k.key, true, &code) == 1) {
+        if (compile_ms)
+            *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return load_module(k.key, code, fn, alpha_fn, err);
+    }
+    if (k.dir.empty() || !read_file(k.dir + "/" + k.name, code)) {
+        bool in_helper = false;
+        std::string compiler;
+        if (!compile(opt, opt.jit_process ? Route::kAuto : Route::kInProcess, source, k.arch, code, err, &compiler,
+                     &in_helper))
+            return false;
+        if (compile_ms)
+            *compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        // (a helper route that fell back to another compiler does not fill the disk cache
+        // under the key of the helper's)
+        if (compiler == route_compiler(opt)) write_file_atomic(k.dir, k.name, code);
+    }
+    return load_module(k.key, code, fn, alpha_fn, err);
+}
+
+JitTry jit_try_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn,
+                      hipFunction_t* alpha_fn, JitTicket* ticket, std::string* err) {
+    KeyInfo k;
+    if (!key_of(opt, device, source, &k, err)) return JitTry::kWait;
+    if (memory_lookup(k.key, fn, alpha_fn)) return JitTry::kReady;
+    std::vector<char> code;
+    const int st = pending_code(k.key, false, &code);
+    if (st == 1) return load_module(k.key, code, fn, alpha_fn, err) ? JitTry::kReady : JitTry::kWait;
+    if (st >= 0) return JitTry::kWait;   // compiling (another solve started it), or failed
+    if (!k.dir.empty() && read_file(k.dir + "/" + k.name, code))
+        return load_module(k.key, code, fn, alpha_fn, err) ? JitTry::kReady : JitTry::kWait;
+    if (!use_helper(opt)) return JitTry::kWait;
+    Pending* p = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_pend_mu);
+        if (g_pending.count(k.key)) return JitTry::kWait;   // (another thread started it meanwhile)
+        p = new Pending;
+        g_pending[k.key] = p;
+    }
+    const std::string helper = helper_path(), dir = k.dir, name = k.name;
+    std::vector<std::string> opts = compile_options(opt, k.arch);
+    try {
+        std::thread([p, helper, opts, source, dir, name]() {
+            std::vector<char> out;
+            std::string e;
+            const bool ok = compile_in_helper(helper, opts, source, out, &e);
+            if (ok) write_file_atomic(dir, name, out);
+            std::lock_guard<std::mutex> lock(g_pend_mu);
+            if (ok) p->code.swap(out);
+            p->state = ok ? 1 : 2;
+            g_pend_cv.notify_all();
+        }).detach();
+    } catch (...) {   // no thread: mark it failed (a blocking compile then)
+        std::lock_guard<std::mutex> lock(g_pend_mu);
+        p->state = 2;
+        g_pend_cv.notify_all();
+        return JitTry::kWait;
+    }
+    if (ticket) ticket->p = p;
+    return JitTry::kStarted;
 }
 
 }  // namespace wost

@@ -56,6 +56,22 @@ std::string jit_generate(const Options& opt, int mode, const DProgram& hdr, cons
 bool jit_get_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn, std::string* err,
                     hipFunction_t* alpha_fn = nullptr, double* compile_ms = nullptr);
 
+// Background compiles for a solve that can run on the precompiled kernel meanwhile
+// (option jit_race, wost_api.hip solve_race): jit_try_kernel returns
+//   kReady   -- *fn is the kernel (in memory, on disk, or a finished background compile);
+//   kStarted -- it was nowhere and nothing compiled it: a compile started now in a helper
+//               process (a detached thread waits for it and fills the disk cache); *ticket
+//               says when it is done, and jit_get_kernel then loads it without compiling;
+//   kWait    -- only a blocking jit_get_kernel gets it (a compile of it is already running,
+//               or failed, or there is no helper).
+enum class JitTry { kReady, kStarted, kWait };
+struct JitTicket {
+    const void* p = nullptr;
+    bool done() const;
+};
+JitTry jit_try_kernel(const Options& opt, int device, const std::string& source, hipFunction_t* fn,
+                      hipFunction_t* alpha_fn, JitTicket* ticket, std::string* err);
+
 // A compile of `source` for `arch` with the options `opt` selects, without a device (the
 // helper process wost_jitc when there is one and opt.jit_process is set, else in this
 // process; *in_helper says which ran). For wost_jit_compile and the tests.

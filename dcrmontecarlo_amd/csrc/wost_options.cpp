@@ -43,6 +43,7 @@ const Spec kSpecs[] = {
     {"philox_ahead", &Options::philox_ahead, nullptr, -1, 3, true, false, "WOST_JIT_PHILOX_AHEAD"},
     {"param_sources", &Options::param_sources, nullptr, 0, 1, true, false, nullptr},
     {"jit_process", &Options::jit_process, nullptr, 0, 1, false, false, nullptr},
+    {"jit_race", &Options::jit_race, nullptr, 0, 1, false, false, nullptr},
     {"chunk0", &Options::chunk0, nullptr, -1, 1024, false, false, "WOST_CHUNK0"},
     {"chunk_min", &Options::chunk_min, nullptr, -1, 1024, false, false, "WOST_CHUNK_MIN"},
     {"chunk_max", &Options::chunk_max, nullptr, -1, 1 << 20, false, false, "WOST_CHUNK_MAX"},

@@ -56,6 +56,8 @@ struct Options {
                                     // program buffer (one compile per source structure; wost_jit.cpp)
     int jit_process = 1;            // compile in the helper process wost_jitc (the same code object;
                                     // concurrent handles' compiles overlap), 0: in this process
+    int jit_race = 1;               // a whole solve whose specialised kernel is in no cache runs on the
+                                    // precompiled kernel while it compiles (wost_api.hip solve_race)
     // work queue (wost_api.hip solve_impl; -1 / 0: the call's own shape)
     int chunk0 = -1;
     int chunk_min = -1;

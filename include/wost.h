@@ -30,7 +30,7 @@ typedef unsigned long long uint64_t;
 extern "C" {
 #endif
 
-#define WOST_ABI_VERSION 5
+#define WOST_ABI_VERSION 6
 
 /* Most source fields one multi-source solve can score (wost_set_sources). */
 #define WOST_MAX_SOURCES 16
@@ -189,6 +189,10 @@ typedef struct {
     double last_wave_ms;
     uint32_t last_wave_iters;
     uint32_t max_wave_iters;
+    /* walks this solve ran on the precompiled kernel while its field-specialised kernel
+     * compiled in the background (option jit_race: only the solve that starts a compile;
+     * the same results either way) */
+    uint64_t precompiled_walks;
 } wost_timing;
 
 int wost_version(void);
@@ -460,7 +464,8 @@ int wost_set_segment_tree(wost_handle* h, int32_t min_segments, int32_t leaf_seg
  * default walk for walk. Names (dcrmontecarlo_amd/csrc/wost_options.h): tree_pool,
  * pool_near, pool_slots, pool_near_waves, pool_min_push, tree_lds, tree_lds_block,
  * tree_share, tree_share_min, tree_share_descent, tree_batch, tree_qmargin, jit_waves,
- * const_vertices, jit_slp, walk_block, fused_scan, refill_min, philox_ahead, param_sources, jit_process, chunk0,
+ * const_vertices, jit_slp, walk_block, fused_scan, refill_min, philox_ahead, param_sources, jit_process, jit_race,
+ * chunk0,
  * chunk_min, chunk_max, adaptive_chunk, grid_blocks_per_cu, lds_pad_bytes.
  * WOST_ERR_INVALID_ARG for an unknown name or a value out of range; WOST_ERR_UNSUPPORTED
  * for a study-build-only name (exp_flags, tree_iter_stats) in the product library. The

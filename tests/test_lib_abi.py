@@ -14,7 +14,7 @@ def test_library_exports_every_declared_symbol():
     assert len(declared) >= 13
     missing = [s for s in declared if not hasattr(_lib.lib, s)]
     assert not missing, missing
-    assert _lib.lib.wost_version() == _lib.ABI_VERSION == 5
+    assert _lib.lib.wost_version() == _lib.ABI_VERSION == 6
 
 
 def test_num_blocks():
@@ -30,7 +30,7 @@ def test_struct_layouts():
     assert ctypes.sizeof(_lib.WostTerm) == 12
     assert ctypes.sizeof(_lib.WostPolyline) == 16
     assert ctypes.sizeof(_lib.WostProblem) == 80
-    assert ctypes.sizeof(_lib.WostTiming) == 120
+    assert ctypes.sizeof(_lib.WostTiming) == 128
 
 
 def test_fails_loudly_without_a_device():
