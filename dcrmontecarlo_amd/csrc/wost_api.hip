@@ -1396,6 +1396,8 @@ void add_timing(wost_timing& acc, const wost_timing& t) {
 // done the specialised kernel runs the rest. Ranges of walks are whole blocks, so the
 // block sums, their order and every output are those of one launch (as wost_solve_range's).
 // A solve that finds the compile already running waits for it instead (jit_get_kernel).
+constexpr double kCompileExpectMs = 300.0;   // a specialised kernel's compile (MI355X box: 180-600 ms)
+
 int solve_race(wost_handle* h, const float* points, int64_t n_points, int64_t W, int32_t max_steps, float eps,
                uint64_t seed, double* block_stats, double* point_stats, float* walk_values, uint32_t* walk_steps) {
     const int64_t nb = wost_num_blocks(n_points, W);
@@ -1426,6 +1428,7 @@ int solve_race(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         return (int64_t)std::min(b, 1e15) * WOST_BLOCK_WALKS;
     };
     int64_t piece = std::min(max_piece, blocks_up((double)(1 << 19) / (double)n_points));
+    const auto race_t0 = std::chrono::steady_clock::now();
     std::vector<double> all((size_t)n_points * nbpp * row), part;
     std::vector<float> pv;
     std::vector<uint32_t> ps;
@@ -1441,8 +1444,11 @@ int solve_race(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         if (walk_steps) ps.resize((size_t)n_points * wc);
         h->jit_enabled = jit_now;
         const auto t0 = std::chrono::steady_clock::now();
-        rc = solve_impl(h, points, n_points, W, 0, 0, max_steps, eps, seed, part.data(), nullptr,
-                        walk_values ? pv.data() : nullptr, walk_steps ? ps.data() : nullptr, nullptr, false, w0, w1);
+        // (the whole range is an ordinary solve: solve_impl takes [0, W) as no range)
+        const bool whole = w0 == 0 && w1 == W;
+        rc = solve_impl(h, points, n_points, W, 0, whole ? nb : 0, max_steps, eps, seed, part.data(), nullptr,
+                        walk_values ? pv.data() : nullptr, walk_steps ? ps.data() : nullptr, nullptr, false, w0,
+                        whole ? -1 : w1);
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         h->jit_enabled = saved;
         if (rc == WOST_ERR_UNSUPPORTED && !jit_now) {   // (a shape only the specialised kernel runs)
@@ -1458,8 +1464,20 @@ int solve_race(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         }
         if (!jit_now) {
             h->timing.precompiled_walks = (uint64_t)(n_points * wc);
-            // the next range: ~16 ms of work at this one's rate, at most 8x larger
-            piece = std::min(max_piece, std::max(piece, std::min(8 * piece, blocks_up((double)wc * 16.0 / std::max(ms, 0.05)))));
+            // the next range, from this one's rate: all the rest when the precompiled kernel
+            // finishes it before the compile is likely done (every range ends in a tail of
+            // the longest walks: one launch, not many); else about half the compile's
+            // expected remaining time, at least 16 ms of work, at most 8x this range
+            const double rate = (double)wc / std::max(ms, 0.05);   // walks per point per ms
+            const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                                                            race_t0).count();
+            const double compile_left = std::max(0.0, kCompileExpectMs - since);
+            if ((double)(W - w1) / rate <= compile_left) {
+                piece = std::min(max_piece, W - w1);
+            } else {
+                const double target = std::max(16.0, 0.5 * compile_left);
+                piece = std::min(max_piece, std::max(piece, std::min(8 * piece, blocks_up(rate * target))));
+            }
         }
         add_timing(acc, h->timing);
         w0 = w1;
