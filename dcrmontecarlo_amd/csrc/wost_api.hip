@@ -11,7 +11,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <map>
+#include <thread>
+#include <set>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -378,28 +381,87 @@ const std::vector<float>& fixed_screened_table() {
 // table is computed once per process (8-14 ms of host time, which every fresh handle's
 // first solve paid; a survey's handles share one sigma_bar). kind 0: Green's, 1: the
 // Jacobian-corrected Green's (compat fixed), 2: screened.
-void sampler_nodes_once(int kind, double sigma_bar, float* out) {
-    static std::mutex mu;
-    static std::map<std::pair<int, uint64_t>, std::vector<float>> cache;
+// (the cache and its lock are never destroyed: a prefetch thread may outlive the statics)
+struct NodeCache {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::pair<int, uint64_t>, std::vector<float>> done;
+    std::set<std::pair<int, uint64_t>> running;
+};
+NodeCache& node_cache() {
+    static NodeCache* c = new NodeCache;
+    return *c;
+}
+
+std::pair<int, uint64_t> node_key(int kind, double sigma_bar) {
     uint64_t bits = 0;
     if (kind == 2) std::memcpy(&bits, &sigma_bar, sizeof(bits));
-    const auto key = std::make_pair(kind, bits);
-    {
-        std::lock_guard<std::mutex> lock(mu);
-        auto it = cache.find(key);
-        if (it != cache.end()) {
-            std::memcpy(out, it->second.data(), sizeof(float) * WOST_SAMPLER_TABLE_N);
-            return;
-        }
-    }
-    std::vector<float> v(WOST_SAMPLER_TABLE_N);
+    return std::make_pair(kind, bits);
+}
+
+void compute_nodes(int kind, double sigma_bar, std::vector<float>& v) {
+    v.resize(WOST_SAMPLER_TABLE_N);
     if (kind == 2) screened_sampler_nodes(v.data(), WOST_SAMPLER_TABLE_N, sigma_bar);
     else if (kind == 1) greens_sampler_nodes_jacobian(v.data(), WOST_SAMPLER_TABLE_N);
     else greens_sampler_nodes(v.data(), WOST_SAMPLER_TABLE_N);
+}
+
+void store_nodes(const std::pair<int, uint64_t>& key, std::vector<float>&& v) {
+    NodeCache& c = node_cache();
+    std::lock_guard<std::mutex> lock(c.mu);
+    if (c.done.size() >= 64) c.done.clear();
+    c.done.emplace(key, std::move(v));
+    c.running.erase(key);
+    c.cv.notify_all();
+}
+
+void sampler_nodes_once(int kind, double sigma_bar, float* out) {
+    NodeCache& c = node_cache();
+    const auto key = node_key(kind, sigma_bar);
+    {
+        std::unique_lock<std::mutex> lock(c.mu);
+        c.cv.wait(lock, [&] { return !c.running.count(key); });   // (a prefetch computing them)
+        auto it = c.done.find(key);
+        if (it != c.done.end()) {
+            std::memcpy(out, it->second.data(), sizeof(float) * WOST_SAMPLER_TABLE_N);
+            return;
+        }
+        c.running.insert(key);
+    }
+    std::vector<float> v;
+    compute_nodes(kind, sigma_bar, v);
     std::memcpy(out, v.data(), sizeof(float) * WOST_SAMPLER_TABLE_N);
-    std::lock_guard<std::mutex> lock(mu);
-    if (cache.size() >= 64) cache.clear();
-    cache.emplace(key, std::move(v));
+    store_nodes(key, std::move(v));
+}
+
+// wost_create: the nodes a first solve of this handle needs, computed in the background
+// while the handle's device setup runs (a fresh process's first HIP calls take ~0.1 s).
+void sampler_nodes_prefetch(int kind, double sigma_bar) {
+    NodeCache& c = node_cache();
+    const auto key = node_key(kind, sigma_bar);
+    {
+        std::lock_guard<std::mutex> lock(c.mu);
+        if (c.running.count(key) || c.done.count(key)) return;
+        c.running.insert(key);
+    }
+    try {
+        std::thread([kind, sigma_bar, key]() {
+            std::vector<float> v;
+            compute_nodes(kind, sigma_bar, v);
+            store_nodes(key, std::move(v));
+        }).detach();
+    } catch (...) {
+        std::vector<float> v;
+        compute_nodes(kind, sigma_bar, v);
+        store_nodes(key, std::move(v));
+    }
+}
+
+// The sampler kind ensure_table builds for a handle.
+int sampler_kind(const wost_handle* h) {
+    if (h->delta && h->compat == WOST_COMPAT_FIXED) return 1;
+    if (h->delta) return 2;
+    return h->compat == WOST_COMPAT_FIXED ? 1 : 0;
 }
 
 int ensure_table(wost_handle* h) {
@@ -410,7 +472,7 @@ int ensure_table(wost_handle* h) {
     const size_t n = table_floats(h->delta, fix_delta);
     h->table.assign(n, 0.f);
     if (fix_delta) {
-        sampler_nodes_once(1, 0.0, h->table.data());   // staged, unused
+        sampler_nodes_once(sampler_kind(h), 0.0, h->table.data());   // staged, unused
         greens_norm_cells(h->table.data() + kSamplerFloatsPadded, kGnormCells, (double)kGnormCells / kGnormInvH);
         const std::vector<float>& fx = fixed_screened_table();
         std::memcpy(h->table.data() + kFixTableOffset, fx.data(), sizeof(float) * fx.size());
@@ -709,10 +771,13 @@ extern "C" {
 
 int wost_create(const wost_problem* pb, wost_handle** out) {
     if (!pb || !out) return fail(WOST_ERR_INVALID_ARG, "NULL argument");
+    jit_start_identity_probe();   // (the compile helper's start, in the background)
     wost_handle* h = nullptr;
     int rc = create_host(pb, &h);
     if (rc != WOST_OK) return rc;
     *out = nullptr;
+    if (h->fields[SLOT_F].present || h->delta)   // the first solve's sampler nodes, meanwhile
+        sampler_nodes_prefetch(sampler_kind(h), h->sigma_bar);
 
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);

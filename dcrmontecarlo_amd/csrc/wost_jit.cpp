@@ -509,24 +509,55 @@ const std::string& helper_path() {
 
 // The hiprtc library the helper compiles with (wost_jitc --identity, run once per
 // process), or "" when there is no helper or it cannot run: compiles stay in this process.
+// wost_create starts the probe in the background (jit_start_identity_probe: ~13 ms of the
+// child's start that then overlaps building the handle); the first compile waits for it.
+std::string run_identity_probe(const std::string& helper) {
+    if (helper.empty()) return std::string();
+    Scratch sc;
+    if (!sc.ok) return std::string();
+    const std::string out = sc.file("identity.txt"), log = sc.file("log.txt");
+    std::string err;
+    std::vector<char> text;
+    if (!run_child({helper, "--identity"}, out, log, &err) || !read_file(out, text)) {
+        std::fprintf(stderr, "libwost: compile helper %s unusable (%s); compiling in this process\n", helper.c_str(),
+                     err.c_str());
+        return std::string();
+    }
+    std::string s(text.begin(), text.end());
+    while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
+    return s;
+}
+
+struct IdentityProbe {   // (never destroyed: its thread may outlive the process's statics)
+    std::mutex mu;
+    std::condition_variable cv;
+    bool started = false, done = false;
+    std::string id;
+};
+IdentityProbe& identity_probe() {
+    static IdentityProbe* p = new IdentityProbe;
+    return *p;
+}
+
+void finish_identity_probe(const std::string& id) {
+    IdentityProbe& p = identity_probe();
+    std::lock_guard<std::mutex> lock(p.mu);
+    p.id = id;
+    p.done = true;
+    p.cv.notify_all();
+}
+
 const std::string& helper_identity() {
-    static const std::string id = [] {
-        if (helper_path().empty()) return std::string();
-        Scratch sc;
-        if (!sc.ok) return std::string();
-        const std::string out = sc.file("identity.txt"), log = sc.file("log.txt");
-        std::string err;
-        std::vector<char> text;
-        if (!run_child({helper_path(), "--identity"}, out, log, &err) || !read_file(out, text)) {
-            std::fprintf(stderr, "libwost: compile helper %s unusable (%s); compiling in this process\n",
-                         helper_path().c_str(), err.c_str());
-            return std::string();
-        }
-        std::string s(text.begin(), text.end());
-        while (!s.empty() && (s.back() == '\n' || s.back() == '\r')) s.pop_back();
-        return s;
-    }();
-    return id;
+    IdentityProbe& p = identity_probe();
+    std::unique_lock<std::mutex> lock(p.mu);
+    if (!p.started) {   // no handle started it: probe here
+        p.started = true;
+        lock.unlock();
+        finish_identity_probe(run_identity_probe(helper_path()));
+        lock.lock();
+    }
+    p.cv.wait(lock, [&p] { return p.done; });
+    return p.id;
 }
 
 bool use_helper(const Options& opt) { return opt.jit_process != 0 && !helper_identity().empty(); }
@@ -652,6 +683,21 @@ bool jit_compile_host(const Options& opt, const std::string& source, const std::
 }
 
 bool jit_helper_available() { return !helper_identity().empty(); }
+
+void jit_start_identity_probe() {
+    IdentityProbe& p = identity_probe();
+    {
+        std::lock_guard<std::mutex> lock(p.mu);
+        if (p.started) return;
+        p.started = true;
+    }
+    const std::string helper = helper_path();
+    try {
+        std::thread([helper]() { finish_identity_probe(run_identity_probe(helper)); }).detach();
+    } catch (...) {
+        finish_identity_probe(run_identity_probe(helper));
+    }
+}
 
 bool jit_const_dirichlet(const Options& o, int nd) { return nd <= o.const_vertices; }
 

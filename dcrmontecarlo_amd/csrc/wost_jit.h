@@ -77,7 +77,10 @@ JitTry jit_try_kernel(const Options& opt, int device, const std::string& source,
 // process; *in_helper says which ran). For wost_jit_compile and the tests.
 bool jit_compile_host(const Options& opt, const std::string& source, const std::string& arch,
                       std::vector<char>* code, std::string* err, bool* in_helper);
-// Whether the compile helper is installed next to this library.
+// Whether the compile helper is installed next to this library (and runs).
 bool jit_helper_available();
+// Starts finding the helper's compiler in the background (once per process; wost_create),
+// so that the first compile does not wait for the helper's start.
+void jit_start_identity_probe();
 
 }  // namespace wost

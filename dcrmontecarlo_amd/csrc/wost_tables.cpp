@@ -2,9 +2,45 @@
 #include "wost_tables.h"
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
 #include <cmath>
 
 namespace wost {
+
+namespace {
+
+// f(i) for i in [0, n) on up to 8 host threads taking chunks of kChunk indices (the sampler
+// tables' nodes and density samples are independent of one another: the same bits as one
+// thread; a fresh process's first delta-tracking solve waited ~60 ms for them on one core).
+template <class F>
+void parallel_for(int n, F f, int kChunk = 64) {
+#if defined(WOST_TABLES_SERIAL)   // (tests/test_tables_parallel.py: the one-thread reference)
+    const int T = 1;
+#else
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int T = (int)std::max(1u, std::min(8u, hw));
+#endif
+    if (T <= 1 || n < 4 * kChunk) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (;;) {
+            const int i0 = next.fetch_add(kChunk);
+            if (i0 >= n) return;
+            for (int i = i0; i < std::min(n, i0 + kChunk); ++i) f(i);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; ++t) th.emplace_back(work);
+    work();
+    for (std::thread& x : th) x.join();
+}
+
+}  // namespace
 
 static const double kPi = 3.14159265358979323846;
 
@@ -136,26 +172,26 @@ void greens_sampler_nodes(float* out, int n) {
     const double c0 = a - a * std::log(a);
     const double z = 1.0 - c0;
     auto cdf = [&](double rho) { return (rho - rho * std::log(rho) - c0) / z; };
-    for (int i = 0; i < n; ++i) {
+    parallel_for(n, [&](int i) {
         const double u = (double)i / (double)(n - 1);
         double lo = a, hi = 1.0;
-        if (i == 0) { out[i] = (float)a; continue; }
-        if (i == n - 1) { out[i] = 1.0f; continue; }
+        if (i == 0) { out[i] = (float)a; return; }
+        if (i == n - 1) { out[i] = 1.0f; return; }
         for (int it = 0; it < 200 && hi - lo > 1e-17; ++it) {
             double mid = 0.5 * (lo + hi);
             if (mid == lo || mid == hi) break;   // adjacent doubles: the bracket no longer moves
             if (cdf(mid) < u) lo = mid; else hi = mid;
         }
         out[i] = (float)(0.5 * (lo + hi));
-    }
+    });
 }
 
 void greens_sampler_nodes_jacobian(float* out, int n) {
     auto cdf = [](double rho) { return rho * rho * (1.0 - 2.0 * std::log(rho)); };
-    for (int i = 0; i < n; ++i) {
+    parallel_for(n, [&](int i) {
         const double u = (double)i / (double)(n - 1);
-        if (i == 0) { out[i] = 0.0f; continue; }
-        if (i == n - 1) { out[i] = 1.0f; continue; }
+        if (i == 0) { out[i] = 0.0f; return; }
+        if (i == n - 1) { out[i] = 1.0f; return; }
         double lo = 0.0, hi = 1.0;
         for (int it = 0; it < 200 && hi - lo > 1e-17; ++it) {
             const double mid = 0.5 * (lo + hi);
@@ -163,7 +199,7 @@ void greens_sampler_nodes_jacobian(float* out, int n) {
             if (cdf(mid) < u) lo = mid; else hi = mid;
         }
         out[i] = (float)(0.5 * (lo + hi));
-    }
+    });
 }
 
 // I0 by its power series (every term positive: no cancellation, ~1 ulp) for x <= 30, where it
@@ -192,17 +228,17 @@ void screened_sampler_nodes(float* out, int n, double sigma_bar) {
     const double kR = k0_host(s), iR = i0_host(s);
     const double ratio = kR / iR;
     std::vector<double> p(J + 1), C(J + 1);
-    for (int j = 0; j <= J; ++j) {
+    parallel_for(J + 1, [&](int j) {
         const double rho = a + j * h;
         const double g = std::fabs((k0_host(rho * s) - ratio * i0_series(rho * s)) / (2.0 * kPi));
         p[j] = std::min(g, M);
-    }
+    });
     C[0] = 0.0;
     for (int j = 0; j < J; ++j) C[j + 1] = C[j] + 0.5 * h * (p[j] + p[j + 1]);
     const double tot = C[J];
-    for (int i = 0; i < n; ++i) {
-        if (i == 0) { out[i] = (float)a; continue; }
-        if (i == n - 1) { out[i] = 1.0f; continue; }
+    parallel_for(n, [&](int i) {
+        if (i == 0) { out[i] = (float)a; return; }
+        if (i == n - 1) { out[i] = 1.0f; return; }
         const double target = tot * (double)i / (double)(n - 1);
         int j = (int)(std::upper_bound(C.begin(), C.end(), target) - C.begin()) - 1;
         j = std::max(0, std::min(j, J - 1));
@@ -211,7 +247,7 @@ void screened_sampler_nodes(float* out, int n, double sigma_bar) {
         const double disc = std::sqrt(std::max(0.0, B * B + 4.0 * A * T));
         const double d = (B + disc) > 0.0 ? 2.0 * T / (B + disc) : 0.0;
         out[i] = (float)(a + j * h + d);
-    }
+    });
 }
 
 // ---------------------------------------------------------------------------
@@ -316,7 +352,7 @@ double screened_fixed_node_u(int i, int cols) {
 }
 
 void screened_fixed_nodes(float* out, int rows, int cols, double xmax) {
-    for (int j = 0; j < rows; ++j) {
+    parallel_for(rows, [&](int j) {
         const ScreenedRow row_law(j == 0 ? 0.0 : std::expm1(xmax * (double)j / (double)(rows - 1)));
         float* row = out + (size_t)j * cols;
         row[0] = 0.0f;
@@ -340,7 +376,7 @@ void screened_fixed_nodes(float* out, int rows, int cols, double xmax) {
             lo0 = lo;
             row[i] = (float)x;
         }
-    }
+    }, 1);
 }
 
 }  // namespace wost
