@@ -35,3 +35,23 @@ def gpu_available():
     if n == 0:
         pytest.fail("no HIP device visible: -m gpu tests must run on an MI355X (no CPU fallback exists)")
     return n
+
+
+@pytest.fixture(autouse=True)
+def _compile_before_first_solve(request, monkeypatch):
+    """GPU tests check the field-specialised kernels -- and each kernel option -- against the
+    oracle, the reference's fixtures and one another, so every solver they build compiles
+    its kernel before its first solve (option jit_race = 0). By default (jit_race = 1) a
+    solve whose kernel is in no cache runs on the precompiled kernel while it compiles: the
+    same bits, tested by tests/test_gpu_race.py, which keeps the default."""
+    if request.node.get_closest_marker("gpu") is None or request.node.fspath.basename == "test_gpu_race.py":
+        return
+    from dcrmontecarlo_amd.solvers import WoStSolver as W
+
+    orig = W.WostSolver_2D.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        self.set_option("jit_race", 0)
+
+    monkeypatch.setattr(W.WostSolver_2D, "__init__", init)
