@@ -641,10 +641,10 @@ bool compile_in_helper(const std::string& helper, const std::vector<std::string>
 
 std::mutex g_inproc_mu;   // at most one compile in this process (comgr serialises them anyway)
 
-// A compile for `arch`. kAuto (handles with jit_process): in this process when no other
-// compile runs here and this process binds the helper's compiler (a lone compile saves the
-// child's start, ~25 ms), else in a helper, so that concurrent compiles overlap; kHelper:
-// in a helper; kInProcess: here. A helper that fails falls back to this process.
+// A compile for `arch`: in a helper (kAuto: handles with jit_process; kHelper), so that
+// concurrent compiles overlap, or here (kInProcess). A helper that fails falls back to
+// this process. (Routing a lone compile here instead saved its child's start, ~25 ms, but
+// made a survey's 34 concurrent compiles 0.6-1.2 s slower: profiles/r06_cold/s23_*.)
 // *compiler: the hiprtc library that compiled (the disk cache only takes code of the
 // compiler its key names).
 bool compile(const Options& opt, Route route, const std::string& src, const std::string& arch,
@@ -652,13 +652,6 @@ bool compile(const Options& opt, Route route, const std::string& src, const std:
     const std::vector<std::string> opts = compile_options(opt, arch);
     *in_helper = false;
     const bool helper = route != Route::kInProcess && !helper_identity().empty();
-    if (helper && route == Route::kAuto && helper_identity() == rtc_library_once()) {
-        std::unique_lock<std::mutex> lock(g_inproc_mu, std::try_to_lock);
-        if (lock.owns_lock()) {
-            *compiler = rtc_library_once();
-            return rtc_compile(src, opts, &code, err);
-        }
-    }
     if (helper) {
         std::string herr;
         if (compile_in_helper(helper_path(), opts, src, code, &herr)) {
