@@ -14,7 +14,9 @@ import sys
 def per_dispatch(d, counter):
     vals = {}
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if "wost_walk" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        # (the field-specialised walk kernel only: a raced first solve also runs the
+        # precompiled wost_walk_kernel on walk ranges, jit_race)
+        if "wost_walk_jit" in r["Kernel_Name"] and r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return list(vals.values())
 
