@@ -107,3 +107,34 @@ def test_no_race_when_the_kernel_is_cached(gpu_available):
     b = sc.solver()
     b.solve(sc.points[:4], nWalks=4096, maxSteps=sc.max_steps, eps=sc.eps, seed=1)
     assert b.last_timing["precompiled_walks"] == 0 and b.last_timing["jit"] == 1
+
+
+@pytest.mark.parametrize("case", ["fixed_poisson", "long_dirichlet"])
+def test_raced_solve_other_kernel_shapes(gpu_available, case):
+    """The race under compat="fixed" (the corrected estimator's kernels) and with a
+    Dirichlet polyline too long to stage (the specialised kernel reads it from global
+    memory, the precompiled one stages it): the same bits as a warm specialised solve."""
+    from dcrmontecarlo_amd.fields import X, Y
+    from dcrmontecarlo_amd.geometry import PolyLinesSimple
+    from dcrmontecarlo_amd.solvers import WostSolver_2D
+
+    k = float(1.0 + np.random.default_rng().uniform(1e-3, 2e-3))   # a kernel new to this process
+    if case == "fixed_poisson":
+        D = np.array([[-1, -1], [1, -1], [1, 1], [-1, 1], [-1, -1]], np.float32)
+        mk = lambda: WostSolver_2D(PolyLinesSimple(D), X**3 + Y**2, source=(-6.0 * X - 2.0) * k, compat="fixed")
+        pts = np.array([[0.1, 0.2], [-0.4, 0.5], [0.7, -0.6]], np.float32)
+    else:
+        t = np.linspace(0.0, 2.0 * np.pi, 6001, dtype=np.float64)
+        D = np.stack([np.cos(t), np.sin(t)], axis=1).astype(np.float32)
+        D[-1] = D[0]
+        mk = lambda: WostSolver_2D(PolyLinesSimple(D), (X**2 - Y**2) * k)
+        pts = np.array([[0.1, 0.2], [-0.5, 0.3], [0.0, -0.7]], np.float32)
+    cold = mk()
+    v0, s0 = cold.solve_walks(pts, nWalks=6000, maxSteps=1000, eps=1e-3, seed=9)
+    assert cold.last_timing["precompiled_walks"] > 0
+    warm = mk()
+    warm.set_option("jit_race", 0)
+    v1, s1 = warm.solve_walks(pts, nWalks=6000, maxSteps=1000, eps=1e-3, seed=9)
+    assert warm.last_timing["jit"] == 1
+    np.testing.assert_array_equal(s0, s1)
+    np.testing.assert_array_equal(v0.view(np.uint32), v1.view(np.uint32))
