@@ -106,6 +106,9 @@ def main():
         best["mean_steps"] = best["steps"] / (npts * W)
         best["first_solve_steps_per_s_kernel"] = t_first["total_steps"] / (t_first["walk_kernel_ms"] * 1e-3)
         best["first_over_best_kernel"] = t_first["walk_kernel_ms"] / best["kernel_ms"]
+        # (a fresh process's first solve of a kernel runs its walks on the precompiled kernel
+        # while the field-specialised one compiles: jit_race)
+        best["first_solve_precompiled_walks"] = int(t_first.get("precompiled_walks", 0))
         best["shape"] = {k: t_first.get(k) for k in ("grid_blocks", "blocks_per_cu", "chunk0", "chunk", "adaptive")}
         best["tail_ms"] = t_first.get("tail_ms")
         best["max_walk_steps"] = t_first.get("max_walk_steps")
