@@ -77,12 +77,12 @@ def test_raced_per_walk_outputs(gpu_available):
 
 
 def test_raced_solve_switches_to_the_specialised_kernel(gpu_available):
-    """A solve long enough to outlast the compile (C4's 48 electrodes x 8M walks: ~1.2 s on
+    """A solve long enough to outlast the compile (C4's 48 electrodes x 16M walks: ~2.6 s on
     the precompiled kernel, a compile takes ~0.3 s): the precompiled kernel runs its first
     ranges, the specialised one the rest, and the point sums are those of one warm solve."""
     rng = np.random.default_rng()
     sc = _fresh("dcr_dipole", rng)
-    W = 8 << 20
+    W = 16 << 20
     cold = sc.solver()
     u0, st0 = cold.solve(sc.points, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=3, return_stats=True)
     t0 = cold.last_timing
