@@ -138,3 +138,24 @@ def test_raced_solve_other_kernel_shapes(gpu_available, case):
     assert warm.last_timing["jit"] == 1
     np.testing.assert_array_equal(s0, s1)
     np.testing.assert_array_equal(v0.view(np.uint32), v1.view(np.uint32))
+
+
+def test_raced_solve_in_ragged_ranges(gpu_available):
+    """Several precompiled ranges and a last range that ends inside a 4096-walk block
+    (48 electrodes x 100,001 walks: the first range is 12,288 walks of every electrode):
+    block sums, their order and the per-walk outputs are one launch's."""
+    rng = np.random.default_rng()
+    sc = _fresh("dcr_dipole", rng)
+    W = 100_001
+    cold = sc.solver()
+    v0, s0 = cold.solve_walks(sc.points, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=21)
+    t0 = cold.last_timing
+    assert t0["precompiled_walks"] > 0 and t0["n_launches"] >= 2, t0
+    warm = _warm(sc)
+    v1, s1 = warm.solve_walks(sc.points, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=21)
+    np.testing.assert_array_equal(s0, s1)
+    np.testing.assert_array_equal(v0.view(np.uint32), v1.view(np.uint32))
+    u0, st0 = sc.solver().solve(sc.points, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=21, return_stats=True)
+    u1, st1 = warm.solve(sc.points, nWalks=W, maxSteps=sc.max_steps, eps=sc.eps, seed=21, return_stats=True)
+    np.testing.assert_array_equal(np.asarray(u0), np.asarray(u1))
+    np.testing.assert_array_equal(st0.stderr, st1.stderr)
