@@ -1293,8 +1293,8 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         const int64_t want = (count + block - 1) / block;
         const int grid = (int)std::max<int64_t>(1, std::min(max_grid, want));
         const int64_t waves = (int64_t)grid * (block / 64);
-        // The work queue (wost_walk.h): static chunks of up to 64 walks per wave (one per
-        // lane), then chunks of the rest from one global counter. Every dequeue of that
+        // The work queue (wost_walk.h): a static chunk of walks per wave (below), then
+        // chunks of the rest from one global counter. Every dequeue of that
         // counter serialises at its address (~11-16 ns): C2's 640k walks took 34k dequeues of
         // 19 walks, all waves hitting the counter at the launch's start, 0.60 ms for 47 us of
         // work (profiles/r05_ab/queue_chunk/, queue_static/).
@@ -1306,7 +1306,16 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         //   kernels' long walks (C5: 208 steps; a wave's last chunk is work no other wave can
         //   take: the survey 1.42e10 -> 1.46e10, profiles/r05_ab/chunk_cap/); each wave then
         //   raises it to the floor its measured walk rate needs (WalkArgs::adaptive).
-        int64_t chunk0 = mode_tree(mode) ? 0 : std::min<int64_t>(64, (count + waves - 1) / waves);
+        // - the static first chunk: at most one walk per lane (64) for long walks; for short
+        //   ones every walk of the launch when that is at most 6 per lane (no wave dequeues at
+        //   all), else 4 per lane (256). C2's 640k walks: 313 per wave, kernel 0.176 ->
+        //   0.129 ms; 12.8M walks of Laplace / Poisson: 256, +12% / +6% (64 took one walk
+        //   per lane and left ~8k dequeues serialised at the counter; profiles/r06_ab/r06s3[12]/)
+        const int64_t per_wave = (count + waves - 1) / waves;
+        int64_t chunk0 = mode_tree(mode)  ? 0
+                         : !short_walks   ? std::min<int64_t>(64, per_wave)
+                         : per_wave <= 384 ? per_wave
+                                           : 256;
         if (O.chunk0 >= 0) chunk0 = O.chunk0;
         const int64_t share = std::max<int64_t>(1, std::min<int64_t>(1 << 20, count / (waves * 4)));
         int64_t chunk_min = short_walks ? 64 : 1;
