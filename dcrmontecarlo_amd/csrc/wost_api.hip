@@ -1283,11 +1283,13 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         const bool short_walks = !mode_neu(mode);
         // Resident workgroups: few short walks per lane (C2: 640k walks, ~1.2 per lane at
         // full occupancy) leave the launch as long as its longest walk chains, whose steps
-        // run faster with fewer waves per SIMD: ~4 walks per lane, at least 2 workgroups per
-        // CU (C2: 0.21 -> 0.18 ms per launch, profiles/r05_ab/grid_c2/)
+        // run faster with fewer waves per SIMD: ~2 walks per lane, at least 2 workgroups per
+        // CU (C2: 8 -> 2 per CU took 0.21 -> 0.18 ms, profiles/r05_ab/grid_c2/; with the
+        // all-static first chunk below 4 per CU beat 2: 0.127 -> 0.110 ms, and 8 stays best
+        // at 4x C2's walks, profiles/r06_ab/r06s37/)
         int64_t bpc = blocks_per_cu;
         if (short_walks && bpc > 2)
-            bpc = std::max<int64_t>(2, std::min<int64_t>(bpc, count / ((int64_t)h->num_cus * block * 4)));
+            bpc = std::max<int64_t>(2, std::min<int64_t>(bpc, count / ((int64_t)h->num_cus * block * 2)));
         if (O.grid_blocks_per_cu > 0) bpc = std::max<int64_t>(1, std::min<int64_t>(blocks_per_cu, O.grid_blocks_per_cu));
         const int64_t max_grid = bpc * h->num_cus;
         const int64_t want = (count + block - 1) / block;
