@@ -230,12 +230,12 @@ struct wost_handle {
     float* d_val = nullptr;
     uint32_t* d_steps = nullptr;
     int64_t ws_cap = 0, ws_val_cap = 0;
-    int64_t* d_begin = nullptr;
-    int64_t begin_cap = 0;
+    int64_t* d_begin = nullptr;       // (d_points and d_begin point into d_stage)
+    char* d_stage = nullptr;          // device image of the pinned staging's [points | block ranges]
+    size_t stage_cap = 0;
     double* d_bstats = nullptr;
     int64_t bstats_cap = 0;
     float2* d_points = nullptr;
-    int64_t points_cap = 0;
     float* d_point_alpha = nullptr;   // alpha at the query points (delta tracking)
     int64_t point_alpha_cap = 0;
     uint32_t* d_pool = nullptr;       // walk pools of the tree kernels' workgroups (WalkArgs::pool)
@@ -689,7 +689,7 @@ void wost_destroy(wost_handle* h) {
     if (!h) return;
     if (h->device >= 0) (void)hipSetDevice(h->device);
     void* ptrs[] = {h->d_dverts, h->d_nverts, h->d_table, h->d_prog, h->d_counter, h->d_val,
-                    h->d_steps, h->d_begin, h->d_bstats, h->d_points, h->d_tree, h->d_seg_phi, h->d_point_alpha, h->d_pool};
+                    h->d_steps, h->d_stage, h->d_bstats, h->d_tree, h->d_seg_phi, h->d_point_alpha, h->d_pool};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
@@ -1062,18 +1062,36 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
     if (range && Wr > batch_limit)
         return fail(WOST_ERR_INVALID_ARG, "walk range of %lld walks per point exceeds one launch (%lld walks)",
                     (long long)Wr, (long long)batch_limit);
-    if ((rc = ensure_cap(h->d_points, h->points_cap, std::max<int64_t>(n_points, 1))) != WOST_OK) return rc;
-    // pinned staging: [points | one batch's block ranges | the block sums], 64-byte aligned
+    // pinned staging: [points | one batch's block ranges | the block sums], 64-byte aligned;
+    // the device holds the first two parts in one buffer of the same layout, so that one copy
+    // brings the points and the first batch's block ranges (C2: a copy and its ~6 us gap less)
     auto al64 = [](size_t b) { return (b + 63) / 64 * 64; };
-    const size_t pin_pts = al64(sizeof(float2) * (size_t)n_points);
+    const size_t pin_pts = al64(sizeof(float2) * (size_t)std::max<int64_t>(n_points, 1));
     const size_t pin_beg = al64(sizeof(int64_t) * (size_t)(nblk + 1));
     const size_t pin_bs = al64(sizeof(double) * (size_t)(kLstatsWords + row * nblk));
     if ((rc = ensure_pin(h, pin_pts + pin_beg + pin_bs)) != WOST_OK) return rc;
+    if (pin_pts + pin_beg > h->stage_cap) {
+        if (h->d_stage) (void)hipFree(h->d_stage);
+        h->d_stage = nullptr;
+        h->stage_cap = 0;
+        const hipError_t e = hipMalloc(&h->d_stage, pin_pts + pin_beg);
+        if (e != hipSuccess)
+            return fail(WOST_ERR_OOM, "hipMalloc(%zu bytes): %s", pin_pts + pin_beg, hipGetErrorString(e));
+        h->stage_cap = pin_pts + pin_beg;
+    }
+    h->d_points = reinterpret_cast<float2*>(h->d_stage);
+    h->d_begin = reinterpret_cast<int64_t*>(h->d_stage + pin_pts);
     float* const pin_points = reinterpret_cast<float*>(h->h_pin);
     int64_t* const pin_begin = reinterpret_cast<int64_t*>(h->h_pin + pin_pts);
     double* const pin_bstats = reinterpret_cast<double*>(h->h_pin + pin_pts + pin_beg);
     std::memcpy(pin_points, points, sizeof(float2) * (size_t)n_points);
-    HIP_TRY(hipMemcpyAsync(h->d_points, pin_points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
+    // the points go with the first batch's block ranges, unless the query points' alpha
+    // (delta tracking) needs them first
+    bool points_pending = true;
+    if (mode_delta(mode) && n_points > 0) {
+        HIP_TRY(hipMemcpyAsync(h->d_points, pin_points, sizeof(float2) * n_points, hipMemcpyHostToDevice, h->stream));
+        points_pending = false;
+    }
     if ((rc = ensure_workspace(h, std::min<int64_t>(walks_total, batch_limit), ns)) != WOST_OK) return rc;
     if ((rc = ensure_cap(h->d_bstats, h->bstats_cap, kLstatsWords + nblk * row)) != WOST_OK) return rc;
     // (the launch statistics in front of the block sums: one copy brings both)
@@ -1262,10 +1280,15 @@ int solve_impl(wost_handle* h, const float* points, int64_t n_points, int64_t W,
         begins.push_back(count);
         const int64_t nb = j2 - j;
 
-        if ((rc = ensure_cap(h->d_begin, h->begin_cap, nb + 1)) != WOST_OK) return rc;
         // (the previous batch's copy from the staging has completed: its events were waited on)
         std::memcpy(pin_begin, begins.data(), sizeof(int64_t) * (size_t)(nb + 1));
-        HIP_TRY(hipMemcpyAsync(h->d_begin, pin_begin, sizeof(int64_t) * (nb + 1), hipMemcpyHostToDevice, h->stream));
+        if (points_pending) {   // points and block ranges in one copy
+            HIP_TRY(hipMemcpyAsync(h->d_stage, h->h_pin, pin_pts + sizeof(int64_t) * (size_t)(nb + 1),
+                                   hipMemcpyHostToDevice, h->stream));
+            points_pending = false;
+        } else {
+            HIP_TRY(hipMemcpyAsync(h->d_begin, pin_begin, sizeof(int64_t) * (nb + 1), hipMemcpyHostToDevice, h->stream));
+        }
         // the queue head: zeroed by the previous launch's block reduce, or here after a
         // solve that stopped between a walk launch and its reduce
         if (!h->counter_zero)

@@ -282,10 +282,19 @@ wost_block_reduce(const float* __restrict__ val, const uint32_t* __restrict__ st
     __shared__ int s_last;
     const int row = 2 * ns + 1;
     if (ctl != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ctl[0] = 0ull;   // (a vector store)
-    if (ctl != nullptr && lstats != nullptr && blockIdx.x == 0)
+    // the waves' records (scan kernels): reduced by one extra workgroup, the last, beside the
+    // block sums (C2: its 4,096 records held up workgroup 0's sums); the segment-tree kernels
+    // keep none (n_waves 0: workgroup 0 writes their empty statistics)
+    const bool stats_wg = ctl != nullptr && lstats != nullptr && n_waves > 0;
+    const int64_t nred = (int64_t)gridDim.x - (stats_wg ? 1 : 0);   // workgroups that sum blocks
+    if (stats_wg && (int64_t)blockIdx.x == nred) {
+        reduce_wave_stats(reinterpret_cast<const uint4*>(ctl + kCtlWords), n_waves, lstats, first_batch);
+        return;
+    }
+    if (!stats_wg && ctl != nullptr && lstats != nullptr && blockIdx.x == 0)
         reduce_wave_stats(reinterpret_cast<const uint4*>(ctl + kCtlWords), n_waves, lstats, first_batch);
     uint32_t mx_all = 0u;
-    for (int64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    for (int64_t b = blockIdx.x; b < nblocks; b += nred) {
         const int64_t lo = begin[b], hi = begin[b + 1];
         for (int k = 0; k < ns; ++k) {
             double s = 0.0, q = 0.0;
@@ -348,7 +357,8 @@ hipError_t launch_block_reduce(const float* val, const uint32_t* steps, const in
                                int64_t nblocks, int ns, double* out, unsigned long long* ctl,
                                hipStream_t s, int64_t n_waves, unsigned long long* lstats, int first_batch) {
     if (nblocks <= 0) return ctl ? hipMemsetAsync(ctl, 0, sizeof(unsigned long long) * kCtlWords, s) : hipSuccess;
-    const int grid = (int)(nblocks < 65536 ? nblocks : 65536);
+    // (one more workgroup for the waves' records: wost_block_reduce)
+    const int grid = (int)(nblocks < 65536 ? nblocks : 65536) + ((ctl && lstats && n_waves > 0) ? 1 : 0);
     wost_block_reduce<<<grid, kReduceBlock, 0, s>>>(val, steps, begin, nblocks, ns, out, ctl, n_waves, lstats,
                                                     first_batch);
     return hipGetLastError();
