@@ -109,9 +109,10 @@ def _load():
         "wost_set_field": (c_int32, [H, c_int32, POINTER(WostField)]),
         "wost_get_info": (c_int32, [H, POINTER(c_double), POINTER(c_int32)]),
         "wost_num_blocks": (c_int64, [c_int64, c_int64]),
-        "wost_solve": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
-                                 c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_float),
-                                 POINTER(c_uint32)]),
+        # (plain addresses: c_void_p takes a pointer object or an int, and the facade's solve
+        # passes the arrays' addresses -- a data_as() pointer costs ~3 us of host time each)
+        "wost_solve": (c_int32, [H, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int32, c_float,
+                                 c_uint64, c_void_p, c_void_p, c_void_p, c_void_p]),
         "wost_solve_history": (c_int32, [H, POINTER(c_float), c_int64, c_int64, c_int32, c_float, c_uint64,
                                          POINTER(c_double), POINTER(c_float), POINTER(c_uint32), POINTER(c_float)]),
         "wost_prepare_sources": (c_int32, [H, POINTER(POINTER(WostField)), c_int32, c_int64]),
@@ -216,6 +217,11 @@ def fptr(a: np.ndarray):
 
 def dptr(a: np.ndarray):
     return a.ctypes.data_as(POINTER(c_double)) if a is not None else None
+
+
+def addr(a: np.ndarray):
+    """The array's data address for a c_void_p argument (None for None)."""
+    return a.__array_interface__["data"][0] if a is not None else None
 
 
 def u32ptr(a: np.ndarray):

@@ -37,6 +37,9 @@ def _is_torch(a) -> bool:
     return type(a).__module__.startswith("torch")
 
 
+_TIMING_FIELDS = tuple(k for k, _ in _lib.WostTiming._fields_)
+
+
 def _points_np(a) -> np.ndarray:
     if _is_torch(a):
         a = a.detach().cpu().numpy()
@@ -330,7 +333,7 @@ class WostSolver_2D:
     def timing(self) -> dict:
         t = _lib.WostTiming()
         _lib.check(_lib.lib.wost_last_timing(self._h, ctypes.byref(t)), "wost_last_timing")
-        return {k: getattr(t, k) for k, _ in _lib.WostTiming._fields_}
+        return {k: getattr(t, k) for k in _TIMING_FIELDS}
 
     def solve(self, solvePoints, nWalks=1000, maxSteps=1000, eps=1e-4, return_history=False, *,
               seed: int = 0, return_stats: bool = False):
@@ -371,8 +374,8 @@ class WostSolver_2D:
                        "WostSolver_2D.solve")
         else:
             nb = self.num_blocks(n, nWalks)
-            _lib.check(_lib.lib.wost_solve(self._h, _lib.fptr(p), n, nWalks, 0, nb, int(maxSteps), float(eps),
-                                           int(seed) & (2**64 - 1), None, _lib.dptr(sums), None, None),
+            _lib.check(_lib.lib.wost_solve(self._h, _lib.addr(p), n, nWalks, 0, nb, int(maxSteps), float(eps),
+                                           int(seed) & (2**64 - 1), None, _lib.addr(sums), None, None),
                        "WostSolver_2D.solve")
         self.last_timing = self.timing()
         self.last_point_sums = sums
