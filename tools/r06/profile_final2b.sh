@@ -4,7 +4,7 @@
 # summaries and PMC passes, one counter group per run -- and the C5 tree kernel's single
 # launch (tools/scenario_bench.py, the bench's speedup_vs_bruteforce sample); then the
 # default bench line, the C2/C3/C5 bench lines and the scenario table. Each step has its own time limit; a crash or timeout ends the session.
-O=gpurun_out/r06prof5b
+O=gpurun_out/r06prof6b
 source "$(dirname "$0")/common.sh"
 export TMPDIR=/tmp
 git_rev="$(cat tools/r06/COMMIT 2>/dev/null || echo unknown)"
